@@ -1,0 +1,10 @@
+"""cdm_amd — MI355X-native (gfx950 HIP) ContextUnet DDPM for 64x64 CAMELS HI maps.
+
+Drop-in for the reference's ContextUnet module API (ContextUnet.py), its diffusion helpers
+(code/train_diffusion_condition.py) and the train_diffusion.py CLI.  Import as ``cdm_amd`` (the
+repo-root ``cdm_amd.py`` shim maps the hyphenated directory to that name).
+"""
+from ._lib import lib  # noqa: F401
+from .model import ContextUnet, EmbedFC, ResidualConvBlock, UnetDown, UnetUp  # noqa: F401
+
+__all__ = ["ContextUnet", "EmbedFC", "ResidualConvBlock", "UnetDown", "UnetUp", "lib"]

@@ -1,0 +1,37 @@
+// Shared definitions for the CDNA4 (gfx950) ContextUnet DDPM kernels.
+// Layout convention: every activation is NHWC fp32; a tensor view is (ptr, N, H, W, C, ldc) where
+// element (n,h,w,c) lives at ptr[((n*H + h)*W + w)*ldc + c].  ldc > C addresses a channel slice of
+// a wider buffer, which is how the reference's torch.cat calls (diffusion_utilities.py:96,
+// ContextUnet.py:59) are eliminated: producers write straight into their slice.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CDM_API extern "C" __attribute__((visibility("default")))
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+static __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+static __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+static __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+static __device__ __forceinline__ float f4get(const float4& v, int j) {
+    return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+
+// exact (erf) GELU, as torch.nn.GELU() default (diffusion_utilities.py:130, ContextUnet.py:17)
+static __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+static __device__ __forceinline__ float gelu_grad_f(float x) {
+    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+    const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
+    return cdf + x * pdf;
+}
+
+static inline int cdm_status() { return (int)hipGetLastError(); }
+
+static __device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}

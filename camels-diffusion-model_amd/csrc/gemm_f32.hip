@@ -1,0 +1,419 @@
+// fp32 MFMA (v_mfma_f32_32x32x2_f32) implicit-GEMM family for gfx950.
+//
+// One templated main loop serves every contraction on the ContextUnet path:
+//   conv3x3 fwd            C[pix][co]      = im2col(X)[pix][tap,ci] . Wp[tap,ci][co]
+//   conv3x3 dgrad          same kernel, X := dY, Wp := flipped/transposed weights
+//   convT 2x2 fwd          C[pix][ij,co]   = X[pix][ci] . Wt[ci][ij,co]        (scatter epilogue)
+//   convT 2x2 dgrad        C[pix][ci]      = gather(dY)[pix][ij,co] . WtT[ij,co][ci]
+//   up0 (convT k=H/4 1x1)  C[n][ij,co]     = hv[n][ci] . W0[ci][ij,co]
+//   *_wgrad (split-K)      C[m][n]         = sum_pix A^T[pix][m] . B[pix][n] -> fp32 partial slabs
+// Reference ops: nn.Conv2d(.,.,3,1,1) diffusion_utilities.py:27,34 / ContextUnet.py:36,39;
+// nn.ConvTranspose2d(in,out,2,2) diffusion_utilities.py:86; ConvTranspose2d(k=h/4) ContextUnet.py:27.
+//
+// Tile: 128x128 per 256-thread workgroup (4 waves as 2x2, each wave 64x64 = 2x2 MFMA 32x32
+// accumulators = 64 AGPRs), BK in {16,32}, LDS double buffer staged through registers (the global
+// loads for tile t+1 are issued before the MFMAs of tile t, written to LDS after them: T14).
+// LDS images are k-major ([k][m], [k][n]) so every MFMA operand read is one conflict-free
+// ds_read_b32 of 32 consecutive floats per half-wave.  Partial-tile bounds are handled by the
+// loaders (zero fill) and the epilogues (masked stores), so any M and N%4==0, K%4==0 work.
+#include "cdm_common.h"
+
+namespace cdm {
+
+constexpr int GBM = 128;
+constexpr int GBN = 128;
+constexpr int GTHREADS = 256;
+
+// ============================== A loaders, k-contiguous: A(m, k..k+3) ==============================
+struct LdDenseA {  // A[m][k] = a[m*lda + k]
+    const float* a; long long lda; int M, K;
+    struct Row { const float* p; };
+    __device__ __forceinline__ Row row(int m) const { return Row{m < M ? a + (long long)m * lda : nullptr}; }
+    __device__ __forceinline__ float4 load(const Row& r, int k) const {
+        return (r.p && k < K) ? ld4(r.p + k) : f4zero();
+    }
+};
+
+struct LdIm2colA {  // 3x3, stride 1, pad 1; m = (n,h,w), k = (ky*3+kx)*C + ci
+    const float* x; int H, W, C, ldx, M, K;
+    struct Row { int n, h, w; bool ok; };
+    __device__ __forceinline__ Row row(int m) const {
+        Row r; r.ok = m < M; const int hw = H * W; r.n = m / hw; const int rem = m - r.n * hw;
+        r.h = rem / W; r.w = rem - r.h * W; return r;
+    }
+    __device__ __forceinline__ float4 load(const Row& r, int k) const {
+        if (!r.ok || k >= K) return f4zero();
+        const int tap = k / C, ci = k - tap * C;
+        const int ky = tap / 3, kx = tap - ky * 3;
+        const int hh = r.h + ky - 1, ww = r.w + kx - 1;
+        if ((unsigned)hh >= (unsigned)H || (unsigned)ww >= (unsigned)W) return f4zero();
+        return ld4(x + ((long long)(r.n * H + hh) * W + ww) * ldx + ci);
+    }
+};
+
+struct LdConvT2x2GatherA {  // dgrad of convT 2x2: m = (n,h,w) on the INPUT grid, k = (i*2+j)*Co + co
+    const float* dy; int H, W, Co, lddy, M, K;   // dy is [N, 2H, 2W, Co] (ld lddy)
+    struct Row { int n, h, w; bool ok; };
+    __device__ __forceinline__ Row row(int m) const {
+        Row r; r.ok = m < M; const int hw = H * W; r.n = m / hw; const int rem = m - r.n * hw;
+        r.h = rem / W; r.w = rem - r.h * W; return r;
+    }
+    __device__ __forceinline__ float4 load(const Row& r, int k) const {
+        if (!r.ok || k >= K) return f4zero();
+        const int ij = k / Co, co = k - ij * Co;
+        const int oh = 2 * r.h + (ij >> 1), ow = 2 * r.w + (ij & 1);
+        return ld4(dy + ((long long)(r.n * 2 * H + oh) * (2 * W) + ow) * lddy + co);
+    }
+};
+
+// ============================== A loader, m-contiguous: A(m..m+3, k) (wgrad) ==============================
+struct LdDenseAT {  // A(m, k) = a[k*lda + m]  (a is [K][M] row-major, e.g. dY[pix][co])
+    const float* a; long long lda; int M, K;
+    __device__ __forceinline__ float4 loadT(int k, int m) const {
+        return (k < K && m < M) ? ld4(a + (long long)k * lda + m) : f4zero();
+    }
+};
+
+// ============================== B loaders, n-contiguous: B(k, n..n+3) ==============================
+struct LdDenseB {  // B[k][n] = b[k*ldb + n]
+    const float* b; long long ldb; int K, N;
+    struct Col { int n; };
+    __device__ __forceinline__ Col col(int n) const { return Col{n}; }
+    __device__ __forceinline__ float4 load(const Col& c, int k) const {
+        return (k < K && c.n < N) ? ld4(b + (long long)k * ldb + c.n) : f4zero();
+    }
+};
+
+struct LdIm2colB {  // conv3x3 wgrad: B(k = pix, n = tap*C + ci) = X[pix shifted by tap][ci]
+    const float* x; int H, W, C, ldx, K, N;
+    struct Col { int dy, dx, ci; bool ok; };
+    __device__ __forceinline__ Col col(int n) const {
+        Col c; c.ok = n < N; const int tap = n / C; c.ci = n - tap * C;
+        const int ky = tap / 3; c.dy = ky - 1; c.dx = tap - ky * 3 - 1; return c;
+    }
+    __device__ __forceinline__ float4 load(const Col& c, int k) const {
+        if (!c.ok || k >= K) return f4zero();
+        const int hw = H * W; const int n = k / hw; const int rem = k - n * hw;
+        const int h = rem / W, w = rem - h * W;
+        const int hh = h + c.dy, ww = w + c.dx;
+        if ((unsigned)hh >= (unsigned)H || (unsigned)ww >= (unsigned)W) return f4zero();
+        return ld4(x + ((long long)(n * H + hh) * W + ww) * ldx + c.ci);
+    }
+};
+
+struct LdConvT2x2GatherB {  // convT 2x2 wgrad: B(k = input pix (n,h,w), n = ij*Co + co) = dY[n,2h+i,2w+j,co]
+    const float* dy; int H, W, Co, lddy, K, N;
+    struct Col { int i, j, co; bool ok; };
+    __device__ __forceinline__ Col col(int n) const {
+        Col c; c.ok = n < N; const int ij = n / Co; c.co = n - ij * Co; c.i = ij >> 1; c.j = ij & 1; return c;
+    }
+    __device__ __forceinline__ float4 load(const Col& c, int k) const {
+        if (!c.ok || k >= K) return f4zero();
+        const int hw = H * W; const int n = k / hw; const int rem = k - n * hw;
+        const int h = rem / W, w = rem - h * W;
+        return ld4(dy + ((long long)(n * 2 * H + 2 * h + c.i) * (2 * W) + 2 * w + c.j) * lddy + c.co);
+    }
+};
+
+// ============================== epilogues ==============================
+// Accumulator element (i, j, r) of a wave sits at row  mw + 32i + (r&3) + 8(r>>2) + 4(lane>>5)
+//                                             column nw + 32j + (lane&31).
+#define CDM_FOR_ACC(...)                                                                   \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                           \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                           \
+    _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                        \
+        const int m = mw + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);              \
+        const int n = nw + 32 * j + (lane & 31);                                             \
+        __VA_ARGS__                                                                          \
+    }
+
+enum { EPI_RELU = 1, EPI_ACCUM = 2 };
+
+struct EpiStore {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-tile column stats
+    float* y; long long ldy; long long zstride; const float* bias; int bias_mod; int flags;
+    float* stats; int stats_ld;  // stats[tile][0|1][stats_ld]: sum / sum of squares of the stored value
+    int M, N;
+
+    __device__ __forceinline__ void operator()(f32x16 (&acc)[2][2], int mw, int nw, int lane, int wm, int wn,
+                                               float* scratch, int tid) const {
+        float* yz = y + (long long)blockIdx.z * zstride;
+        float cs[2] = {0.f, 0.f}, cq[2] = {0.f, 0.f};
+        CDM_FOR_ACC({
+            if (m < M && n < N) {
+                float v = acc[i][j][r];
+                if (bias) v += bias[n % bias_mod];
+                float* p = yz + (long long)m * ldy + n;
+                if (flags & EPI_ACCUM) v += *p;
+                if (flags & EPI_RELU) v = fmaxf(v, 0.f);
+                *p = v;
+                cs[j] += v; cq[j] += v * v;
+            }
+        })
+        if (!stats) return;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) { cs[j] += __shfl_xor(cs[j], 32, 64); cq[j] += __shfl_xor(cq[j], 32, 64); }
+        __syncthreads();  // scratch aliases the operand LDS
+        if (lane < 32) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int c = wn * 64 + 32 * j + lane;
+                scratch[(wm * 2 + 0) * GBN + c] = cs[j];
+                scratch[(wm * 2 + 1) * GBN + c] = cq[j];
+            }
+        }
+        __syncthreads();
+        if (tid < GBN) {
+            const int n = blockIdx.y * GBN + tid;
+            if (n < N) {
+                float* st = stats + (long long)blockIdx.x * 2 * stats_ld;
+                st[n] = scratch[0 * GBN + tid] + scratch[2 * GBN + tid];
+                st[stats_ld + n] = scratch[1 * GBN + tid] + scratch[3 * GBN + tid];
+            }
+        }
+    }
+};
+
+struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n, 2h+i, 2w+j, co] = acc + b[co]
+    float* y; long long ldy; const float* bias; int H, W, Co, M, N;
+    __device__ __forceinline__ void operator()(f32x16 (&acc)[2][2], int mw, int nw, int lane, int, int,
+                                               float*, int) const {
+        CDM_FOR_ACC({
+            if (m < M && n < N) {
+                const int hw = H * W; const int b = m / hw; const int rem = m - b * hw;
+                const int h = rem / W, w = rem - h * W;
+                const int ij = n / Co, co = n - ij * Co;
+                float v = acc[i][j][r] + (bias ? bias[co] : 0.f);
+                y[((long long)(b * 2 * H + 2 * h + (ij >> 1)) * (2 * W) + 2 * w + (ij & 1)) * ldy + co] = v;
+            }
+        })
+    }
+};
+
+// ============================== the main loop ==============================
+template <class LA, class LB, class EP, bool A_MCONTIG, int BK>
+__global__ __launch_bounds__(GTHREADS, 2) void gemm_f32_kernel(LA la, LB lb, EP ep, int K, int kt_per_split) {
+    constexpr int PADA = A_MCONTIG ? 4 : 2;   // k-major A image: stride == 2 (mod 32) -> conflict-free b32 transpose writes
+    constexpr int SA = GBM + PADA, SB = GBN + 4;
+    constexpr int A_LD = GBM * BK / 4 / GTHREADS;
+    constexpr int B_LD = GBN * BK / 4 / GTHREADS;
+    constexpr int TPR = BK / 4;               // threads per A row in the k-contiguous loader
+    __shared__ __attribute__((aligned(16))) float smem[2 * BK * SA + 2 * BK * SB];
+    float (*As)[BK][SA] = reinterpret_cast<float (*)[BK][SA]>(smem);
+    float (*Bs)[BK][SB] = reinterpret_cast<float (*)[BK][SB]>(smem + 2 * BK * SA);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int m0 = blockIdx.x * GBM, n0 = blockIdx.y * GBN;
+    const int ktiles = (K + BK - 1) / BK;
+    const int kt0 = blockIdx.z * kt_per_split;
+    const int kt1 = min(ktiles, kt0 + kt_per_split);
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    float4 ra[A_LD], rb[B_LD];
+    // per-thread fixed coordinates
+    typename LB::Col bcol = lb.col(n0 + (tid % 32) * 4);
+    auto gload = [&](int kt) {
+        const int k0 = kt * BK;
+        if constexpr (!A_MCONTIG) {
+#pragma unroll
+            for (int i = 0; i < A_LD; ++i) {
+                const int rr = tid / TPR + i * (GTHREADS / TPR);
+                const typename LA::Row row = la.row(m0 + rr);
+                ra[i] = la.load(row, k0 + (tid % TPR) * 4);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < A_LD; ++i) ra[i] = la.loadT(k0 + tid / 32 + i * 8, m0 + (tid % 32) * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) rb[i] = lb.load(bcol, k0 + tid / 32 + i * 8);
+    };
+    auto sstore = [&](int buf) {
+        if constexpr (!A_MCONTIG) {
+#pragma unroll
+            for (int i = 0; i < A_LD; ++i) {
+                const int rr = tid / TPR + i * (GTHREADS / TPR), kq = (tid % TPR) * 4;
+                As[buf][kq + 0][rr] = ra[i].x; As[buf][kq + 1][rr] = ra[i].y;
+                As[buf][kq + 2][rr] = ra[i].z; As[buf][kq + 3][rr] = ra[i].w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < A_LD; ++i) st4(&As[buf][tid / 32 + i * 8][(tid % 32) * 4], ra[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) st4(&Bs[buf][tid / 32 + i * 8][(tid % 32) * 4], rb[i]);
+    };
+
+    if (kt0 < kt1) { gload(kt0); sstore(0); }
+    __syncthreads();
+    int cur = 0;
+    const int am = wm * 64 + (lane & 31), bn = wn * 64 + (lane & 31), kh = lane >> 5;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) gload(kt + 1);
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 2) {
+            const float a0 = As[cur][kk + kh][am], a1 = As[cur][kk + kh][am + 32];
+            const float b0 = Bs[cur][kk + kh][bn], b1 = Bs[cur][kk + kh][bn + 32];
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        if (more) sstore(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    ep(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, smem, tid);
+}
+
+template <class LA, class LB, class EP, bool A_MCONTIG, int BK = 16>
+static int launch_gemm(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits, hipStream_t s) {
+    const int ktiles = (K + BK - 1) / BK;
+    if (splits < 1) splits = 1;
+    if (splits > ktiles) splits = ktiles > 0 ? ktiles : 1;
+    const int per = (ktiles + splits - 1) / splits;
+    splits = ktiles > 0 ? (ktiles + per - 1) / per : 1;
+    dim3 grid((M + GBM - 1) / GBM, (N + GBN - 1) / GBN, splits);
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, EP, A_MCONTIG, BK>), grid, dim3(GTHREADS), 0, s, la, lb, ep, K, per);
+    return cdm_status();
+}
+
+// split count actually used by launch_gemm for a requested value (host helper, mirrored in Python)
+static int effective_splits(int K, int splits, int BK = 16) {
+    const int ktiles = (K + BK - 1) / BK;
+    if (splits < 1) splits = 1;
+    if (splits > ktiles) splits = ktiles > 0 ? ktiles : 1;
+    const int per = (ktiles + splits - 1) / splits;
+    return ktiles > 0 ? (ktiles + per - 1) / per : 1;
+}
+
+// ============================== slab reduction / permutation ==============================
+// out[m*s_m + (n / csplit)*s_hi + (n % csplit)*s_lo] (+)= sum_z slab[z][m][n]
+__global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N, float* out,
+                                   long long s_m, long long s_hi, long long s_lo, int csplit, int accumulate,
+                                   float scale) {
+    const long long total = (long long)M * N;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        float v = 0.f;
+        for (int z = 0; z < splits; ++z) v += slab[(long long)z * total + idx];
+        v *= scale;
+        const int m = (int)(idx / N), n = (int)(idx - (long long)m * N);
+        const int hi = n / csplit, lo = n - hi * csplit;
+        float* p = out + m * s_m + hi * s_hi + lo * s_lo;
+        *p = accumulate ? *p + v : v;
+    }
+}
+
+}  // namespace cdm
+
+using namespace cdm;
+
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------------------------------------
+// C ABI (declared in include/cdm_hip.h)
+// ---------------------------------------------------------------------------------------------
+CDM_API int cdm_conv3x3_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,
+                            const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
+                            void* stream) {
+    if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
+    const int M = N * H * W, K = 9 * Cin;
+    LdIm2colA la{x, H, W, Cin, ldx, M, K};
+    LdDenseB lb{wpk, Cout, K, Cout};
+    EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout};
+    return launch_gemm<LdIm2colA, LdDenseB, EpiStore, false>(la, lb, ep, M, Cout, K, 1, S(stream));
+}
+
+CDM_API int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,
+                             const float* bias, float* y, int ldy, int Cout, void* stream) {
+    if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
+    const int M = N * H * W, K = Cin, NN = 4 * Cout;
+    LdDenseA la{x, ldx, M, K};
+    LdDenseB lb{wpk, NN, K, NN};
+    EpiConvT2x2 ep{y, ldy, bias, H, W, Cout, M, NN};
+    return launch_gemm<LdDenseA, LdDenseB, EpiConvT2x2, false>(la, lb, ep, M, NN, K, 1, S(stream));
+}
+
+// dX[n,h,w,ci] (+)= sum_{ij,co} dY[n,2h+i,2w+j,co] * W[ci][co][ij];  H, W are the INPUT (small) grid
+CDM_API int cdm_convT2x2_dgrad(const float* dy, int N, int H, int W, int Cout, int lddy, const float* wpkT,
+                               float* dx, int lddx, int Cin, int flags, void* stream) {
+    if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
+    const int M = N * H * W, K = 4 * Cout;
+    LdConvT2x2GatherA la{dy, H, W, Cout, lddy, M, K};
+    LdDenseB lb{wpkT, Cin, K, Cin};
+    EpiStore ep{dx, lddx, 0, nullptr, 1, flags, nullptr, 0, M, Cin};
+    return launch_gemm<LdConvT2x2GatherA, LdDenseB, EpiStore, false>(la, lb, ep, M, Cin, K, 1, S(stream));
+}
+
+// C[m][n] = A[m][k] . B[k][n] (+bias[n % bias_mod]).  splits > 1: writes raw partials to slab[z][M][N].
+CDM_API int cdm_gemm_f32(const float* a, long long lda, int M, int K, const float* b, long long ldb, int N,
+                         float* c, long long ldc, const float* bias, int bias_mod, int flags, int splits,
+                         float* slab, void* stream) {
+    if (K % 4 || N % 4) return (int)hipErrorInvalidValue;
+    LdDenseA la{a, lda, M, K};
+    LdDenseB lb{b, ldb, K, N};
+    const int sp = effective_splits(K, splits);
+    if (sp > 1) {
+        EpiStore ep{slab, N, (long long)M * N, nullptr, 1, 0, nullptr, 0, M, N};
+        return launch_gemm<LdDenseA, LdDenseB, EpiStore, false>(la, lb, ep, M, N, K, sp, S(stream));
+    }
+    EpiStore ep{c, ldc, 0, bias, bias_mod > 0 ? bias_mod : 1, flags, nullptr, 0, M, N};
+    return launch_gemm<LdDenseA, LdDenseB, EpiStore, false>(la, lb, ep, M, N, K, 1, S(stream));
+}
+
+CDM_API int cdm_gemm_splits(int K, int splits) { return effective_splits(K, splits); }
+
+// slab[z][co][tap*Cin+ci] = partial sum over a pixel range of dY[pix][co] * X[pix+tap][ci]
+CDM_API int cdm_conv3x3_wgrad(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,
+                              int ldx, int splits, float* slab, void* stream) {
+    if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
+    const int M = Cout, NN = 9 * Cin, K = N * H * W;
+    LdDenseAT la{dy, lddy, M, K};
+    LdIm2colB lb{x, H, W, Cin, ldx, K, NN};
+    const int sp = effective_splits(K, splits);
+    EpiStore ep{slab, NN, (long long)M * NN, nullptr, 1, 0, nullptr, 0, M, NN};
+    return launch_gemm<LdDenseAT, LdIm2colB, EpiStore, true>(la, lb, ep, M, NN, K, sp, S(stream));
+}
+
+// slab[z][ci][ij*Cout+co] = partial over input pixels of X[pix][ci] * dY[n,2h+i,2w+j,co]
+CDM_API int cdm_convT2x2_wgrad(const float* x, int N, int H, int W, int Cin, int ldx, const float* dy, int Cout,
+                               int lddy, int splits, float* slab, void* stream) {
+    if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
+    const int M = Cin, NN = 4 * Cout, K = N * H * W;
+    LdDenseAT la{x, ldx, M, K};
+    LdConvT2x2GatherB lb{dy, H, W, Cout, lddy, K, NN};
+    const int sp = effective_splits(K, splits);
+    EpiStore ep{slab, NN, (long long)M * NN, nullptr, 1, 0, nullptr, 0, M, NN};
+    return launch_gemm<LdDenseAT, LdConvT2x2GatherB, EpiStore, true>(la, lb, ep, M, NN, K, sp, S(stream));
+}
+
+// slab[z][m][n] = partial over k of a[k][m] * b[k][n]   (A^T B; up0 / Linear weight gradients)
+CDM_API int cdm_gemm_tn_f32(const float* a, long long lda, int M, int K, const float* b, long long ldb, int N,
+                            int splits, float* slab, void* stream) {
+    if (M % 4 || N % 4) return (int)hipErrorInvalidValue;
+    LdDenseAT la{a, lda, M, K};
+    LdDenseB lb{b, ldb, K, N};
+    const int sp = effective_splits(K, splits);
+    EpiStore ep{slab, N, (long long)M * N, nullptr, 1, 0, nullptr, 0, M, N};
+    return launch_gemm<LdDenseAT, LdDenseB, EpiStore, true>(la, lb, ep, M, N, K, sp, S(stream));
+}
+
+CDM_API int cdm_slab_reduce(const float* slab, int splits, int M, int N, float* out, long long s_m, long long s_hi,
+                            long long s_lo, int csplit, int accumulate, float scale, void* stream) {
+    const long long total = (long long)M * N;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, S(stream), slab, splits, M, N, out, s_m, s_hi,
+                       s_lo, csplit > 0 ? csplit : N, accumulate, scale);
+    return cdm_status();
+}

@@ -1,0 +1,653 @@
+// Small / HBM-bound kernels of the ContextUnet DDPM hot path (gfx950).
+//
+//   conv3x3 with C_in = 1   init_conv.conv1 (diffusion_utilities.py:27 via ContextUnet.py:14)
+//   conv3x3 with C_out = 1  out.3 (ContextUnet.py:39)
+//   AvgPool2d(h/4) + GELU   to_vec (ContextUnet.py:17)
+//   EmbedFC x4              Linear -> GELU -> Linear (diffusion_utilities.py:118-145)
+//   perturb_input           code/train_diffusion_condition.py:202-203
+//   F.mse_loss (+grad)      code/train_diffusion_condition.py:227
+//   denoise_add_noise + CFG code/train_diffusion_condition.py:274-279,318-329 (+ on-device snapshots :331-332)
+//   torch.optim.Adam        code/train_diffusion_condition.py:200 (single-tensor Adam arithmetic)
+//   weight repacking        OIHW / [Cin][Cout][kh][kw] -> GEMM-ready layouts (+ eval-mode BN fold)
+#include "cdm_common.h"
+
+namespace cdm {
+
+static inline int nblocks(long long total, int per = 256, int cap = 8192) {
+    long long b = (total + per - 1) / per;
+    if (b > cap) b = cap;
+    if (b < 1) b = 1;
+    return (int)b;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Philox4x32-10 (counter-based; used for training noise / timesteps and sampler z)
+// ------------------------------------------------------------------------------------------------
+struct U4 { uint32_t x, y, z, w; };
+static __device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                            uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0, hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return U4{c0, c1, c2, c3};
+}
+static __device__ __forceinline__ float u01(uint32_t v) { return ((float)(v >> 8) + 0.5f) * (1.0f / 16777216.0f); }
+static __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
+    const float u1 = u01(a), u2 = u01(b);
+    const float r = sqrtf(-2.0f * logf(u1));
+    float s, c; sincosf(6.283185307179586f * u2, &s, &c);
+    z0 = r * c; z1 = r * s;
+}
+// normal for element e of stream `sub`
+static __device__ __forceinline__ float philox_normal(unsigned long long seed, uint32_t sub, long long e) {
+    const U4 v = philox((uint32_t)(e >> 2), (uint32_t)((unsigned long long)e >> 34), sub, 0x5EEDu,
+                        (uint32_t)seed, (uint32_t)(seed >> 32));
+    float z0, z1, z2, z3;
+    box_muller(v.x, v.y, z0, z1); box_muller(v.z, v.w, z2, z3);
+    const int j = (int)(e & 3);
+    return j == 0 ? z0 : (j == 1 ? z1 : (j == 2 ? z2 : z3));
+}
+
+__global__ void philox_uniform_kernel(float* out, long long n, float lo, float hi, unsigned long long seed, uint32_t sub) {
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q * 4 < n; q += (long long)gridDim.x * blockDim.x) {
+        const U4 v = philox((uint32_t)q, (uint32_t)((unsigned long long)q >> 32), sub, 0x0417u, (uint32_t)seed,
+                            (uint32_t)(seed >> 32));
+        const uint32_t r[4] = {v.x, v.y, v.z, v.w};
+        for (int j = 0; j < 4; ++j) if (q * 4 + j < n) out[q * 4 + j] = lo + (hi - lo) * u01(r[j]);
+    }
+}
+
+__global__ void philox_normal_kernel(float* out, long long n, unsigned long long seed, uint32_t sub) {
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q * 4 < n; q += (long long)gridDim.x * blockDim.x) {
+        const U4 v = philox((uint32_t)q, (uint32_t)((unsigned long long)q >> 32), sub, 0x5EEDu, (uint32_t)seed,
+                            (uint32_t)(seed >> 32));
+        float z[4];
+        box_muller(v.x, v.y, z[0], z[1]); box_muller(v.z, v.w, z[2], z[3]);
+        for (int j = 0; j < 4; ++j) if (q * 4 + j < n) out[q * 4 + j] = z[j];
+    }
+}
+
+// t[n] in [lo, hi] uniformly (torch.randint(1, T+1) equivalent distribution)
+__global__ void philox_randint_kernel(int* out, int n, int lo, int hi, unsigned long long seed, uint32_t sub) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const U4 v = philox((uint32_t)i, 0x71u, sub, 0xA11Cu, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint64_t r = ((uint64_t)v.x << 32) | v.y;
+    out[i] = lo + (int)(r % (uint64_t)(hi - lo + 1));
+}
+
+// ------------------------------------------------------------------------------------------------
+// conv3x3, C_in = 1:  y[p][co] = b[co] + sum_tap x[p+tap] * wt[tap][co]   (wt = pack_conv3x3 output, Cin = 1)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv_cin1_fwd_kernel(const float* x, int N, int H, int W, const float* w9,
+                                                            const float* bias, float* y, int ldy, int C, int relu) {
+    const int C4 = C >> 2;
+    const long long total = (long long)N * H * W * C4;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int c4 = (int)(idx % C4) * 4;
+        const long long pix = idx / C4;
+        const int n = (int)(pix / (H * W)), rem = (int)(pix - (long long)n * H * W), h = rem / W, w = rem - h * W;
+        float xv[9];
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
+            xv[tap] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? x[((long long)n * H + hh) * W + ww] : 0.f;
+        }
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float s = 0.f;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) s = fmaf(xv[tap], w9[tap * C + c4 + j], s);
+            s += bias[c4 + j];
+            o[j] = relu ? fmaxf(s, 0.f) : s;
+        }
+        st4(y + pix * ldy + c4, make_float4(o[0], o[1], o[2], o[3]));
+    }
+}
+
+// per-(n, chunk) partials R = 10: r<9 -> sum dy[p][c]*x[p+tap_r], r=9 -> sum dy[p][c]
+__global__ __launch_bounds__(256) void conv_cin1_wgrad_kernel(const float* dy, int lddy, const float* x, int H, int W,
+                                                              int C, int csize, float* slab) {
+    constexpr int R = 10;
+    __shared__ float red[256 * 4 * R];
+    const int C4 = C >> 2, P = 256 / C4, tid = threadIdx.x, c4 = (tid % C4) * 4, pl = tid / C4;
+    const int n = blockIdx.y, chunk = blockIdx.x, HW = H * W;
+    const int p0 = chunk * csize, p1 = min(HW, p0 + csize);
+    float acc[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[r][j] = 0.f;
+    if (pl < P) {
+        for (int p = p0 + pl; p < p1; p += P) {
+            const int h = p / W, w = p - h * W;
+            const float4 g = ld4(dy + ((long long)n * HW + p) * lddy + c4);
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
+                const float xv = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? x[(long long)n * HW + hh * W + ww] : 0.f;
+                acc[tap][0] += g.x * xv; acc[tap][1] += g.y * xv; acc[tap][2] += g.z * xv; acc[tap][3] += g.w * xv;
+            }
+            acc[9][0] += g.x; acc[9][1] += g.y; acc[9][2] += g.z; acc[9][3] += g.w;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) st4(&red[(pl * R + r) * C + c4], make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]));
+    }
+    __syncthreads();
+    float* out = slab + ((long long)n * gridDim.x + chunk) * R * C;
+    for (int idx = tid; idx < R * C; idx += 256) {
+        float s = 0.f;
+        for (int q = 0; q < P; ++q) s += red[q * R * C + idx];
+        out[idx] = s;
+    }
+}
+
+// out[r*s_r + c*s_c] (+)= sum_t slab[t][r0+r][c]  for r < rn
+__global__ void slab_sum_all_kernel(const float* slab, int ntiles, int R, int r0, int rn, int C, float* out,
+                                    long long s_r, long long s_c, int accumulate) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= rn * C) return;
+    const int r = idx / C, c = idx - r * C;
+    double s = 0.0;
+    for (int t = 0; t < ntiles; ++t) s += slab[((long long)t * R + r0 + r) * C + c];
+    float* p = out + r * s_r + c * s_c;
+    *p = accumulate ? *p + (float)s : (float)s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// conv3x3, C_out = 1 (out.3):  eps[p] = b + sum_{tap,ci} z[p+tap][ci] * w[ci][tap]   (w == OIHW[0] flattened)
+// One wave per 64 consecutive pixels; the C channels are split over 4 waves and reduced in LDS.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv_cout1_fwd_kernel(const float* z, int ldz, int N, int H, int W, int C,
+                                                             const float* w, const float* bias, float* out) {
+    extern __shared__ __attribute__((aligned(16))) float sh[];
+    float* ws = sh;                 // [9][C]  (tap-major)
+    float* part = sh + 9 * C;       // [4][64]
+    for (int i = threadIdx.x; i < 9 * C; i += 256) { const int tap = i / C, ci = i - tap * C; ws[i] = w[ci * 9 + tap]; }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long pix = (long long)blockIdx.x * 64 + lane;
+    const long long P = (long long)N * H * W;
+    float s = 0.f;
+    if (pix < P) {
+        const int n = (int)(pix / (H * W)), rem = (int)(pix - (long long)n * H * W), h = rem / W, wx = rem - h * W;
+        for (int tap = 0; tap < 9; ++tap) {
+            const int hh = h + tap / 3 - 1, ww = wx + tap % 3 - 1;
+            if ((unsigned)hh >= (unsigned)H || (unsigned)ww >= (unsigned)W) continue;
+            const float* zp = z + (((long long)n * H + hh) * W + ww) * ldz;
+            const float* wt = ws + tap * C;
+            for (int c = wv * 4; c < C; c += 16) {
+                const float4 v = ld4(zp + c);
+                s = fmaf(v.x, wt[c], s); s = fmaf(v.y, wt[c + 1], s); s = fmaf(v.z, wt[c + 2], s); s = fmaf(v.w, wt[c + 3], s);
+            }
+        }
+    }
+    part[wv * 64 + lane] = s;
+    __syncthreads();
+    if (wv == 0 && pix < P) out[pix] = part[lane] + part[64 + lane] + part[128 + lane] + part[192 + lane] + bias[0];
+}
+
+// dz[p'][ci] = sum_tap deps[p' - tap + 1] * w[ci][tap]
+__global__ __launch_bounds__(256) void conv_cout1_dgrad_kernel(const float* deps, int N, int H, int W, int C,
+                                                               const float* w, float* dz, int lddz) {
+    const int C4 = C >> 2;
+    const long long total = (long long)N * H * W * C4;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int c4 = (int)(idx % C4) * 4;
+        const long long pix = idx / C4;
+        const int n = (int)(pix / (H * W)), rem = (int)(pix - (long long)n * H * W), h = rem / W, wx = rem - h * W;
+        float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int hh = h - (tap / 3 - 1), ww = wx - (tap % 3 - 1);
+            if ((unsigned)hh >= (unsigned)H || (unsigned)ww >= (unsigned)W) continue;
+            const float g = deps[((long long)n * H + hh) * W + ww];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = fmaf(g, w[(c4 + j) * 9 + tap], o[j]);
+        }
+        st4(dz + pix * lddz + c4, make_float4(o[0], o[1], o[2], o[3]));
+    }
+}
+
+// partials R = 9: r = tap: sum_p deps[p] * z[p+tap][c]
+__global__ __launch_bounds__(256) void conv_cout1_wgrad_kernel(const float* deps, const float* z, int ldz, int H,
+                                                               int W, int C, int csize, float* slab) {
+    constexpr int R = 9;
+    __shared__ float red[256 * 4 * R];
+    const int C4 = C >> 2, P = 256 / C4, tid = threadIdx.x, c4 = (tid % C4) * 4, pl = tid / C4;
+    const int n = blockIdx.y, chunk = blockIdx.x, HW = H * W;
+    const int p0 = chunk * csize, p1 = min(HW, p0 + csize);
+    float acc[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[r][j] = 0.f;
+    if (pl < P) {
+        for (int p = p0 + pl; p < p1; p += P) {
+            const int h = p / W, w = p - h * W;
+            const float g = deps[(long long)n * HW + p];
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
+                if ((unsigned)hh >= (unsigned)H || (unsigned)ww >= (unsigned)W) continue;
+                const float4 v = ld4(z + ((long long)n * HW + hh * W + ww) * ldz + c4);
+                acc[tap][0] += g * v.x; acc[tap][1] += g * v.y; acc[tap][2] += g * v.z; acc[tap][3] += g * v.w;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) st4(&red[(pl * R + r) * C + c4], make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]));
+    }
+    __syncthreads();
+    float* out = slab + ((long long)n * gridDim.x + chunk) * R * C;
+    for (int idx = tid; idx < R * C; idx += 256) {
+        float s = 0.f;
+        for (int q = 0; q < P; ++q) s += red[q * R * C + idx];
+        out[idx] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// AvgPool2d(h/4) + GELU
+// ------------------------------------------------------------------------------------------------
+__global__ void avgpool_gelu_fin_kernel(const float* sums, int N, int C, float inv_hw, float* hpre, float* hv) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N * C) return;
+    const float m = sums[i] * inv_hw;
+    hpre[i] = m; hv[i] = gelu_f(m);
+}
+// dst[n,p,c] += dhv[n][c] * gelu'(hpre[n][c]) / HW
+__global__ void avgpool_gelu_bwd_kernel(const float* dhv, const float* hpre, int N, int HW, int C, float inv_hw,
+                                       float* dst, int ldd) {
+    const int C4 = C >> 2;
+    const long long total = (long long)N * HW * C4;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int c4 = (int)(idx % C4) * 4;
+        const long long pix = idx / C4;
+        const int n = (int)(pix / HW);
+        float4 d = ld4(dst + pix * ldd + c4);
+        float v[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = n * C + c4 + j;
+            v[j] += dhv[k] * gelu_grad_f(hpre[k]) * inv_hw;
+        }
+        st4(dst + pix * ldd + c4, make_float4(v[0], v[1], v[2], v[3]));
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// EmbedFC x4:  out = W2 gelu(W1 x + b1) + b2    (one launch for all four MLPs)
+// ------------------------------------------------------------------------------------------------
+struct MlpDesc {
+    const float* x; int rows; int in_dim; int E;
+    const float* w1; const float* b1; const float* w2; const float* w2t; const float* b2;
+    float* pre; float* h; float* out;
+    const float* dout; float* dpre; float* dw1; float* db1; float* dw2; float* db2;
+};
+struct Mlp4 { MlpDesc m[4]; };
+
+__global__ __launch_bounds__(256) void embed_fwd_kernel(Mlp4 P) {
+    const MlpDesc& d = P.m[blockIdx.y];
+    const int b = blockIdx.x;
+    if (b >= d.rows) return;
+    __shared__ float hs[1024];
+    for (int j = threadIdx.x; j < d.E; j += 256) {
+        float s = d.b1[j];
+        for (int k = 0; k < d.in_dim; ++k) s = fmaf(d.w1[j * d.in_dim + k], d.x[b * d.in_dim + k], s);
+        const float g = gelu_f(s);
+        if (d.pre) { d.pre[(long long)b * d.E + j] = s; d.h[(long long)b * d.E + j] = g; }
+        hs[j] = g;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < d.E; j += 256) {
+        float s = 0.f;
+        for (int i = 0; i < d.E; ++i) s = fmaf(d.w2t[(long long)i * d.E + j], hs[i], s);
+        d.out[(long long)b * d.E + j] = s + d.b2[j];
+    }
+}
+
+// dpre[b][i] = gelu'(pre[b][i]) * sum_j dout[b][j] w2[j][i]
+__global__ __launch_bounds__(256) void embed_bwd_act_kernel(Mlp4 P) {
+    const MlpDesc& d = P.m[blockIdx.y];
+    const int b = blockIdx.x;
+    if (b >= d.rows) return;
+    for (int i = threadIdx.x; i < d.E; i += 256) {
+        float s = 0.f;
+        for (int j = 0; j < d.E; ++j) s = fmaf(d.dout[(long long)b * d.E + j], d.w2[(long long)j * d.E + i], s);
+        d.dpre[(long long)b * d.E + i] = s * gelu_grad_f(d.pre[(long long)b * d.E + i]);
+    }
+}
+
+// parameter grads (assign): dw2[j][i], db2[j], dw1[i][k], db1[i]
+__global__ __launch_bounds__(256) void embed_bwd_param_kernel(Mlp4 P) {
+    const MlpDesc& d = P.m[blockIdx.y];
+    const int E = d.E, I = d.in_dim, rows = d.rows;
+    const long long n_w2 = (long long)E * E, n_all = n_w2 + E + (long long)E * I + E;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n_all;
+         idx += (long long)gridDim.x * blockDim.x) {
+        double s = 0.0;
+        if (idx < n_w2) {
+            const int j = (int)(idx / E), i = (int)(idx - (long long)j * E);
+            for (int b = 0; b < rows; ++b) s += (double)d.dout[(long long)b * E + j] * d.h[(long long)b * E + i];
+            d.dw2[idx] = (float)s;
+        } else if (idx < n_w2 + E) {
+            const int j = (int)(idx - n_w2);
+            for (int b = 0; b < rows; ++b) s += d.dout[(long long)b * E + j];
+            d.db2[j] = (float)s;
+        } else if (idx < n_w2 + E + (long long)E * I) {
+            const long long q = idx - n_w2 - E;
+            const int i = (int)(q / I), k = (int)(q - (long long)i * I);
+            for (int b = 0; b < rows; ++b) s += (double)d.dpre[(long long)b * E + i] * d.x[b * I + k];
+            d.dw1[q] = (float)s;
+        } else {
+            const int i = (int)(idx - n_w2 - E - (long long)E * I);
+            for (int b = 0; b < rows; ++b) s += d.dpre[(long long)b * E + i];
+            d.db1[i] = (float)s;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// diffusion elementwise math
+// ------------------------------------------------------------------------------------------------
+// x_pert = sqrt(ab[t]) x + (1 - ab[t]) noise ; temb_in = float(t)/float(T)
+__global__ void perturb_kernel(const float* x, const float* noise, const int* t, const float* sab, const float* omab,
+                               int N, int HW, float T, float* out, float* tin) {
+    const long long total = (long long)N * HW;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+        const int n = (int)(i / HW);
+        const int ti = t[n];
+        out[i] = sab[ti] * x[i] + omab[ti] * noise[i];
+        if (tin && i - (long long)n * HW == 0) tin[n] = (float)ti / T;
+    }
+}
+
+// per-block partials: [0] sum (pred-noise)^2, [1] sum dpred ; dpred = 2(pred-noise)/numel
+__global__ __launch_bounds__(256) void mse_kernel(const float* pred, const float* noise, long long n, float scale,
+                                                  float* dpred, float* partial) {
+    float s0 = 0.f, s1 = 0.f;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const float d = pred[i] - noise[i];
+        const float g = d * scale;
+        dpred[i] = g;
+        s0 += d * d; s1 += g;
+    }
+    __shared__ float r0[4], r1[4];
+    s0 = wave_sum(s0); s1 = wave_sum(s1);
+    if ((threadIdx.x & 63) == 0) { r0[threadIdx.x >> 6] = s0; r1[threadIdx.x >> 6] = s1; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        partial[blockIdx.x * 2 + 0] = r0[0] + r0[1] + r0[2] + r0[3];
+        partial[blockIdx.x * 2 + 1] = r1[0] + r1[1] + r1[2] + r1[3];
+    }
+}
+// loss = sum0 / numel (written to loss_out), dbias = sum1 (written to dbias_out)
+__global__ void mse_finalize_kernel(const float* partial, int nb, double inv_numel, float* loss_out, float* dbias_out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double a = 0.0, b = 0.0;
+    for (int i = 0; i < nb; ++i) { a += partial[2 * i]; b += partial[2 * i + 1]; }
+    if (loss_out) *loss_out = (float)(a * inv_numel);
+    if (dbias_out) *dbias_out = (float)b;
+}
+
+// Sampler step prologue (device-side step counter, so one captured step replays for every i):
+//   i = *ctr; *ctr = i - 1; cur[0] = i; t_cur = (float)((double)i / T); shortcut rows for step i.
+__global__ void sample_prologue_kernel(int* ctr, int T, int* cur_i, float* t_cur, const float* sc_table, int sc_row,
+                                       float* sc_cur) {
+    const int i = *ctr;
+    __syncthreads();
+    if (threadIdx.x == 0) { *ctr = i - 1; *cur_i = i; *t_cur = (float)((double)i / (double)T); }
+    if (sc_table)
+        for (int k = threadIdx.x; k < sc_row; k += blockDim.x) sc_cur[k] = sc_table[(long long)(T - i) * sc_row + k];
+}
+
+// x <- (x - eps*coef[i]) / sa[i] + sb[i]*z ;  eps = eu + w (ec - eu) when cfg (model batch = 2n)
+// z = 0 at i == 1; z from z_table[(T-i)][e] when given, else Philox(seed, stream i).
+// Writes x into both halves of the model-input buffer (x2 may alias x), and a snapshot when slot[i] >= 0.
+__global__ void denoise_kernel(float* x, float* x2, long long numel, const float* eps, int cfg, float w,
+                               const int* cur_i, const float* coef, const float* sa, const float* sb,
+                               const float* z_table, unsigned long long seed, const int* snap_slot, float* snaps, int T) {
+    const int i = *cur_i;
+    const float cf = coef[i], a = sa[i], b = sb[i];
+    const int slot = snap_slot ? snap_slot[i] : -1;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < numel; e += (long long)gridDim.x * blockDim.x) {
+        float ep = eps[e];
+        if (cfg) { const float eu = eps[numel + e]; ep = eu + w * (ep - eu); }
+        float z = 0.f;
+        if (i > 1) z = z_table ? z_table[(long long)(T - i) * numel + e] : philox_normal(seed, (uint32_t)i, e);
+        const float mean = (x[e] - ep * cf) / a;
+        const float v = mean + b * z;
+        x[e] = v;
+        if (x2) { x2[e] = v; x2[numel + e] = v; }
+        if (slot >= 0) snaps[(long long)slot * numel + e] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Adam (torch single-tensor arithmetic), lr/step in device memory so a captured step replays.
+// state: [0] lr, [1] step (float count), [2] -step_size, [3] sqrt(bias_correction2)
+// ------------------------------------------------------------------------------------------------
+__global__ void adam_prep_kernel(float* state, double beta1, double beta2) {
+    const double step = (double)state[1] + 1.0;
+    state[1] = (float)step;
+    const double bc1 = 1.0 - pow(beta1, step), bc2 = 1.0 - pow(beta2, step);
+    state[2] = (float)(-(double)state[0] / bc1);
+    state[3] = (float)sqrt(bc2);
+}
+__global__ void adam_kernel(float* p, const float* g, float* m, float* v, long long n, const float* state, float beta1c,
+                            float beta2, float beta2c, float eps) {
+    const float nss = state[2], bc2s = state[3];
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const float gi = g[i];
+        float mi = m[i];
+        mi = mi + beta1c * (gi - mi);                    // exp_avg.lerp_(grad, 1 - beta1)
+        float vi = v[i] * beta2;                          // exp_avg_sq.mul_(beta2)
+        vi = vi + beta2c * gi * gi;                       //           .addcmul_(grad, grad, 1 - beta2)
+        const float denom = sqrtf(vi) / bc2s + eps;       // (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
+        p[i] = p[i] + nss * (mi / denom);                 // param.addcdiv_(exp_avg, denom, -step_size)
+        m[i] = mi; v[i] = vi;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight packing
+// ------------------------------------------------------------------------------------------------
+// conv3x3 OIHW W[co][ci][tap] ->  wpk[(tap*Cin + ci)*Cout + co] (* fold[co]),  wdg[(tap*Cout+co)*Cin+ci] = W[co][ci][8-tap]
+// fold (eval BN): s = gamma/sqrt(rv+eps), bpk = (b - rm)*s + beta
+__global__ void pack_conv3x3_kernel(const float* W, const float* b, int Cin, int Cout, const float* gamma,
+                                    const float* beta, const float* rm, const float* rv, float eps, float* wpk,
+                                    float* bpk, float* wdg) {
+    const long long total = (long long)Cout * Cin * 9;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int tap = (int)(idx % 9);
+        const long long q = idx / 9;
+        const int ci = (int)(q % Cin), co = (int)(q / Cin);
+        const float wv = W[idx];
+        float s = 1.f;
+        if (gamma) s = gamma[co] / sqrtf(rv[co] + eps);
+        if (wpk) wpk[((long long)tap * Cin + ci) * Cout + co] = wv * s;
+        if (wdg) wdg[((long long)(8 - tap) * Cout + co) * Cin + ci] = wv;
+        if (bpk && idx < Cout) {
+            const int c = (int)idx;
+            bpk[c] = gamma ? (b[c] - rm[c]) * (gamma[c] / sqrtf(rv[c] + eps)) + beta[c] : b[c];
+        }
+    }
+}
+
+// ConvTranspose weight W[ci][co][kk] ->  wt[ci][kk*Cout + co],  wtT[(kk*Cout + co)][ci]
+__global__ void pack_convT_kernel(const float* W, int Cin, int Cout, int KK, float* wt, float* wtT) {
+    const long long total = (long long)Cin * Cout * KK;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int kk = (int)(idx % KK);
+        const long long q = idx / KK;
+        const int co = (int)(q % Cout), ci = (int)(q / Cout);
+        const float v = W[idx];
+        const long long col = (long long)kk * Cout + co;
+        if (wt) wt[(long long)ci * KK * Cout + col] = v;
+        if (wtT) wtT[col * Cin + ci] = v;
+    }
+}
+
+// out[c][r] = in[r][c]
+__global__ void transpose_kernel(const float* in, int R, int C, float* out) {
+    const long long total = (long long)R * C;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int r = (int)(idx / C), c = (int)(idx - (long long)r * C);
+        out[(long long)c * R + r] = in[idx];
+    }
+}
+
+}  // namespace cdm
+
+using namespace cdm;
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------ C ABI ------------------------------------------------
+CDM_API int cdm_philox_normal(float* out, long long n, unsigned long long seed, unsigned int sub, void* stream) {
+    hipLaunchKernelGGL(philox_normal_kernel, dim3(nblocks((n + 3) / 4)), dim3(256), 0, S(stream), out, n, seed, sub);
+    return cdm_status();
+}
+CDM_API int cdm_philox_uniform(float* out, long long n, float lo, float hi, unsigned long long seed, unsigned int sub,
+                               void* stream) {
+    hipLaunchKernelGGL(philox_uniform_kernel, dim3(nblocks((n + 3) / 4)), dim3(256), 0, S(stream), out, n, lo, hi, seed, sub);
+    return cdm_status();
+}
+CDM_API int cdm_philox_randint(int* out, int n, int lo, int hi, unsigned long long seed, unsigned int sub, void* stream) {
+    hipLaunchKernelGGL(philox_randint_kernel, dim3((n + 255) / 256), dim3(256), 0, S(stream), out, n, lo, hi, seed, sub);
+    return cdm_status();
+}
+CDM_API int cdm_conv3x3_cin1_fwd(const float* x, int N, int H, int W, const float* w9, const float* bias, float* y,
+                                 int ldy, int C, int relu, void* stream) {
+    if (C % 4) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(conv_cin1_fwd_kernel, dim3(nblocks((long long)N * H * W * (C / 4))), dim3(256), 0, S(stream), x, N,
+                       H, W, w9, bias, y, ldy, C, relu);
+    return cdm_status();
+}
+CDM_API int cdm_conv3x3_cin1_wgrad(const float* dy, int lddy, const float* x, int N, int H, int W, int C, int csize,
+                                   float* slab, void* stream) {
+    if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(conv_cin1_wgrad_kernel, dim3((H * W + csize - 1) / csize, N), dim3(256), 0, S(stream), dy, lddy, x,
+                       H, W, C, csize, slab);
+    return cdm_status();
+}
+CDM_API int cdm_slab_sum_all(const float* slab, int ntiles, int R, int r0, int rn, int C, float* out, long long s_r,
+                             long long s_c, int accumulate, void* stream) {
+    hipLaunchKernelGGL(slab_sum_all_kernel, dim3((rn * C + 255) / 256), dim3(256), 0, S(stream), slab, ntiles, R, r0, rn, C,
+                       out, s_r, s_c, accumulate);
+    return cdm_status();
+}
+CDM_API int cdm_conv3x3_cout1_fwd(const float* z, int ldz, int N, int H, int W, int C, const float* w, const float* bias,
+                                  float* out, void* stream) {
+    if (C % 4) return (int)hipErrorInvalidValue;
+    const long long P = (long long)N * H * W;
+    const size_t shm = (size_t)(9 * C + 256) * sizeof(float);
+    hipLaunchKernelGGL(conv_cout1_fwd_kernel, dim3((unsigned)((P + 63) / 64)), dim3(256), shm, S(stream), z, ldz, N, H, W,
+                       C, w, bias, out);
+    return cdm_status();
+}
+CDM_API int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int C, const float* w, float* dz, int lddz,
+                                    void* stream) {
+    if (C % 4) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(conv_cout1_dgrad_kernel, dim3(nblocks((long long)N * H * W * (C / 4))), dim3(256), 0, S(stream),
+                       deps, N, H, W, C, w, dz, lddz);
+    return cdm_status();
+}
+CDM_API int cdm_conv3x3_cout1_wgrad(const float* deps, const float* z, int ldz, int N, int H, int W, int C, int csize,
+                                    float* slab, void* stream) {
+    if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(conv_cout1_wgrad_kernel, dim3((H * W + csize - 1) / csize, N), dim3(256), 0, S(stream), deps, z,
+                       ldz, H, W, C, csize, slab);
+    return cdm_status();
+}
+CDM_API int cdm_avgpool_gelu_fin(const float* sums, int N, int C, int HW, float* hpre, float* hv, void* stream) {
+    hipLaunchKernelGGL(avgpool_gelu_fin_kernel, dim3((N * C + 255) / 256), dim3(256), 0, S(stream), sums, N, C,
+                       1.0f / (float)HW, hpre, hv);
+    return cdm_status();
+}
+CDM_API int cdm_avgpool_gelu_bwd(const float* dhv, const float* hpre, int N, int HW, int C, float* dst, int ldd,
+                                 void* stream) {
+    if (C % 4) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(avgpool_gelu_bwd_kernel, dim3(nblocks((long long)N * HW * (C / 4))), dim3(256), 0, S(stream), dhv,
+                       hpre, N, HW, C, 1.0f / (float)HW, dst, ldd);
+    return cdm_status();
+}
+CDM_API int cdm_embed_fwd(const Mlp4* P, void* stream) {
+    int rows = 1;
+    for (int k = 0; k < 4; ++k) { rows = P->m[k].rows > rows ? P->m[k].rows : rows; if (P->m[k].E > 1024) return (int)hipErrorInvalidValue; }
+    hipLaunchKernelGGL(embed_fwd_kernel, dim3(rows, 4), dim3(256), 0, S(stream), *P);
+    return cdm_status();
+}
+CDM_API int cdm_embed_bwd(const Mlp4* P, void* stream) {
+    int rows = 1;
+    for (int k = 0; k < 4; ++k) rows = P->m[k].rows > rows ? P->m[k].rows : rows;
+    hipLaunchKernelGGL(embed_bwd_act_kernel, dim3(rows, 4), dim3(256), 0, S(stream), *P);
+    int e = cdm_status(); if (e) return e;
+    hipLaunchKernelGGL(embed_bwd_param_kernel, dim3(256, 4), dim3(256), 0, S(stream), *P);
+    return cdm_status();
+}
+CDM_API int cdm_perturb(const float* x, const float* noise, const int* t, const float* sab, const float* omab, int N,
+                        int HW, int T, float* out, float* tin, void* stream) {
+    hipLaunchKernelGGL(perturb_kernel, dim3(nblocks((long long)N * HW)), dim3(256), 0, S(stream), x, noise, t, sab, omab, N,
+                       HW, (float)T, out, tin);
+    return cdm_status();
+}
+CDM_API int cdm_mse(const float* pred, const float* noise, long long n, float* dpred, float* partial, int nb,
+                    float* loss_out, float* dbias_out, void* stream) {
+    hipLaunchKernelGGL(mse_kernel, dim3(nb), dim3(256), 0, S(stream), pred, noise, n, (float)(2.0 / (double)n), dpred,
+                       partial);
+    int e = cdm_status(); if (e) return e;
+    hipLaunchKernelGGL(mse_finalize_kernel, dim3(1), dim3(64), 0, S(stream), partial, nb, 1.0 / (double)n, loss_out,
+                       dbias_out);
+    return cdm_status();
+}
+CDM_API int cdm_sample_prologue(int* ctr, int T, int* cur_i, float* t_cur, const float* sc_table, int sc_row, float* sc_cur,
+                                void* stream) {
+    hipLaunchKernelGGL(sample_prologue_kernel, dim3(1), dim3(256), 0, S(stream), ctr, T, cur_i, t_cur, sc_table, sc_row,
+                       sc_cur);
+    return cdm_status();
+}
+CDM_API int cdm_denoise(float* x, float* x2, long long numel, const float* eps, int cfg, float w, const int* cur_i,
+                        const float* coef, const float* sa, const float* sb, const float* z_table,
+                        unsigned long long seed, const int* snap_slot, float* snaps, int T, void* stream) {
+    hipLaunchKernelGGL(denoise_kernel, dim3(nblocks(numel)), dim3(256), 0, S(stream), x, x2, numel, eps, cfg, w, cur_i, coef,
+                       sa, sb, z_table, seed, snap_slot, snaps, T);
+    return cdm_status();
+}
+CDM_API int cdm_adam(float* p, const float* g, float* m, float* v, long long n, float* state, double beta1, double beta2,
+                     double eps, void* stream) {
+    hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, S(stream), state, beta1, beta2);
+    int e = cdm_status(); if (e) return e;
+    hipLaunchKernelGGL(adam_kernel, dim3(nblocks(n, 256, 16384)), dim3(256), 0, S(stream), p, g, m, v, n, state,
+                       (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps);
+    return cdm_status();
+}
+CDM_API int cdm_pack_conv3x3(const float* W, const float* b, int Cin, int Cout, const float* gamma, const float* beta,
+                             const float* rm, const float* rv, float eps, float* wpk, float* bpk, float* wdg,
+                             void* stream) {
+    hipLaunchKernelGGL(pack_conv3x3_kernel, dim3(nblocks((long long)Cout * Cin * 9)), dim3(256), 0, S(stream), W, b, Cin,
+                       Cout, gamma, beta, rm, rv, eps, wpk, bpk, wdg);
+    return cdm_status();
+}
+CDM_API int cdm_pack_convT(const float* W, int Cin, int Cout, int KK, float* wt, float* wtT, void* stream) {
+    hipLaunchKernelGGL(pack_convT_kernel, dim3(nblocks((long long)Cin * Cout * KK)), dim3(256), 0, S(stream), W, Cin, Cout,
+                       KK, wt, wtT);
+    return cdm_status();
+}
+CDM_API int cdm_transpose(const float* in, int R, int C, float* out, void* stream) {
+    hipLaunchKernelGGL(transpose_kernel, dim3(nblocks((long long)R * C)), dim3(256), 0, S(stream), in, R, C, out);
+    return cdm_status();
+}
+CDM_API int cdm_device_sync() { return (int)hipDeviceSynchronize(); }
+CDM_API int cdm_abi_version() { return 1; }

@@ -1,0 +1,531 @@
+// Normalisation, pooling and FiLM kernels (HBM-bound, float4 over channels, NHWC).
+//
+// Reference ops covered (diffusion_utilities.py / ContextUnet.py):
+//   BatchNorm2d + ReLU            diffusion_utilities.py:28-29,35-36  (train: batch stats, eval: running stats)
+//   random 1x1 shortcut + add     diffusion_utilities.py:54-55
+//   MaxPool2d(2)                  diffusion_utilities.py:109
+//   GroupNorm(8) + ReLU           ContextUnet.py:28-29,37-38
+//   FiLM  cemb*h + temb           ContextUnet.py:57-58
+//
+// Statistics are produced as per-(image, chunk-of-pixels) partial sums in an fp32 "slab"
+// [N][nchunks][R][C] (the conv epilogue writes the same layout with R = 2 and 128-pixel chunks),
+// then folded in fp64 by a tiny finalize kernel.  Deterministic: no atomics anywhere.
+#include "cdm_common.h"
+
+namespace cdm {
+
+struct NormP {              // z_pre = y*s + t ; xhat = (y - mean)*invstd
+    const float* s; const float* t; int sn;                  // index n*sn + c
+    const float* mean; const float* invstd; int mn; int cpg;  // index n*mn + c/cpg
+};
+struct FilmP { const float* a; int an; const float* b; int bn; };  // out = a[n*an+c]*u + b[n*bn+c]
+struct ResidP { const float* x; const float* w; const float* b; int split; };  // + w[c]*x[n,p] + b[c] (C_in = 1)
+
+// -------------------------------------------------------------------------------------------------
+// generic per-(n,c) partial reduction over pixel chunks
+// -------------------------------------------------------------------------------------------------
+template <int R>
+struct Acc4 { float4 v[R]; };
+
+struct StatsF {  // R=2: sum, sum of squares
+    static constexpr int R = 2;
+    const float* y; int ldy; int HW;
+    __device__ __forceinline__ void operator()(int n, int p, int c, Acc4<2>& a) const {
+        const float4 v = ld4(y + ((long long)n * HW + p) * ldy + c);
+        a.v[0].x += v.x; a.v[0].y += v.y; a.v[0].z += v.z; a.v[0].w += v.w;
+        a.v[1].x += v.x * v.x; a.v[1].y += v.y * v.y; a.v[1].z += v.z * v.z; a.v[1].w += v.w * v.w;
+    }
+};
+
+struct SumF {  // R=1: plain sum (bias gradients)
+    static constexpr int R = 1;
+    const float* g; int ldg; int HW;
+    __device__ __forceinline__ void operator()(int n, int p, int c, Acc4<1>& a) const {
+        const float4 v = ld4(g + ((long long)n * HW + p) * ldg + c);
+        a.v[0].x += v.x; a.v[0].y += v.y; a.v[0].z += v.z; a.v[0].w += v.w;
+    }
+};
+
+// Recompute one element's forward pieces.
+static __device__ __forceinline__ void norm_elem(const NormP& np, int n, int c, float y, float& zpre, float& xhat) {
+    zpre = y * np.s[n * np.sn + c] + np.t[n * np.sn + c];
+    const int gi = n * np.mn + c / np.cpg;
+    xhat = (y - np.mean[gi]) * np.invstd[gi];
+}
+
+// R=5 backward sums for  out = [pool|film]( relu( norm(y) ) ):
+//   S1 = sum g_pre, S2 = sum g_pre*xhat, S3 = sum g_out*u (FiLM), S4 = sum g_out (FiLM), S5 = sum xhat
+template <bool POOL, bool FILM>
+struct NormBwdF {
+    static constexpr int R = 5;
+    const float* g; int ldg;      // grad wrt the op output (pooled grid when POOL)
+    const float* y; int ldy;      // pre-norm activations (full grid)
+    int H, W;                     // full grid
+    NormP np; FilmP fp;
+    __device__ __forceinline__ void operator()(int n, int p, int c4, Acc4<5>& a) const {
+        float* acc = reinterpret_cast<float*>(a.v);  // acc[r*4 + j]
+        if constexpr (POOL) {
+            const int Wo = W >> 1, ho = p / Wo, wo = p - ho * Wo;
+            const float4 gv = ld4(g + ((long long)n * (H >> 1) * Wo + p) * ldg + c4);
+            float4 yv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                yv[e] = ld4(y + ((long long)(n * H + 2 * ho + (e >> 1)) * W + 2 * wo + (e & 1)) * ldy + c4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = c4 + j;
+                float zp[4], xh[4], best = -INFINITY; int arg = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    norm_elem(np, n, c, f4get(yv[e], j), zp[e], xh[e]);
+                    const float z = fmaxf(zp[e], 0.f);
+                    if (z > best || isnan(z)) { best = z; arg = e; }
+                }
+                const float gj = f4get(gv, j);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float gpre = (e == arg && zp[e] > 0.f) ? gj : 0.f;
+                    acc[0 * 4 + j] += gpre; acc[1 * 4 + j] += gpre * xh[e]; acc[4 * 4 + j] += xh[e];
+                }
+            }
+        } else {
+            const float4 gv = ld4(g + ((long long)n * H * W + p) * ldg + c4);
+            const float4 yv = ld4(y + ((long long)n * H * W + p) * ldy + c4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = c4 + j;
+                float zp, xh; norm_elem(np, n, c, f4get(yv, j), zp, xh);
+                float gz = f4get(gv, j);
+                if constexpr (FILM) {
+                    const float u = fmaxf(zp, 0.f);
+                    acc[2 * 4 + j] += gz * u; acc[3 * 4 + j] += gz;
+                    gz *= fp.a[n * fp.an + c];
+                }
+                const float gpre = zp > 0.f ? gz : 0.f;
+                acc[0 * 4 + j] += gpre; acc[1 * 4 + j] += gpre * xh; acc[4 * 4 + j] += xh;
+            }
+        }
+    }
+};
+
+// grid (nchunks, N); block 256.  Covers pixels [chunk*csize, min(HWp, ...)) of image n.
+template <class F>
+__global__ __launch_bounds__(256) void chan_reduce_kernel(F f, int HWp, int C, int csize, float* slab) {
+    constexpr int R = F::R;
+    __shared__ float red[256 * 4 * R];
+    const int C4 = C >> 2;
+    const int P = 256 / C4;
+    const int tid = threadIdx.x, c4 = tid % C4, pl = tid / C4;
+    const int n = blockIdx.y, chunk = blockIdx.x;
+    const int p0 = chunk * csize, p1 = min(HWp, p0 + csize);
+    Acc4<R> a;
+#pragma unroll
+    for (int r = 0; r < R; ++r) a.v[r] = f4zero();
+    if (pl < P)
+        for (int p = p0 + pl; p < p1; p += P) f(n, p, c4 * 4, a);
+    // LDS tree over the P pixel lanes
+    if (pl < P) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) st4(&red[(pl * R + r) * C + c4 * 4], a.v[r]);
+    }
+    __syncthreads();
+    float* out = slab + ((long long)n * gridDim.x + chunk) * R * C;
+    for (int idx = tid; idx < R * C; idx += 256) {
+        float s = 0.f;
+        for (int q = 0; q < P; ++q) s += red[q * R * C + idx];
+        out[idx] = s;
+    }
+}
+
+template <class F>
+static int launch_reduce(const F& f, int N, int HWp, int C, int csize, float* slab, hipStream_t s) {
+    if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
+    const int nchunks = (HWp + csize - 1) / csize;
+    hipLaunchKernelGGL(chan_reduce_kernel<F>, dim3(nchunks, N), dim3(256), 0, s, f, HWp, C, csize, slab);
+    return cdm_status();
+}
+
+// -------------------------------------------------------------------------------------------------
+// finalize kernels (fp64 folding of the slabs)
+// -------------------------------------------------------------------------------------------------
+// BatchNorm (train): per channel over all ntiles = N*nchunks partials.  Updates running stats like
+// torch (momentum 0.1, unbiased running var), increments num_batches_tracked (int64) once.
+__global__ void bn_fwd_finalize_kernel(const float* slab, int ntiles, int R, int C, double count,
+                                       const float* gamma, const float* beta, float* rmean, float* rvar,
+                                       long long* nbt, float momentum, float eps, float* mean, float* invstd,
+                                       float* scale, float* shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0 && nbt) *nbt += 1;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int t = 0; t < ntiles; ++t) {
+        s += slab[((long long)t * R + 0) * C + c];
+        q += slab[((long long)t * R + 1) * C + c];
+    }
+    const double mu = s / count;
+    double var = q / count - mu * mu;
+    if (var < 0.0) var = 0.0;
+    const float is = (float)(1.0 / sqrt(var + (double)eps));
+    mean[c] = (float)mu; invstd[c] = is;
+    const float sc = gamma[c] * is;
+    scale[c] = sc; shift[c] = beta[c] - (float)mu * sc;
+    if (rmean) {
+        const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+        rmean[c] = (float)((double)momentum * mu + (1.0 - (double)momentum) * (double)rmean[c]);
+        rvar[c] = (float)((double)momentum * unb + (1.0 - (double)momentum) * (double)rvar[c]);
+    }
+}
+
+// BatchNorm (eval): scale/shift from running stats.
+__global__ void bn_eval_coeffs_kernel(int C, const float* gamma, const float* beta, const float* rmean,
+                                      const float* rvar, float eps, float* mean, float* invstd, float* scale,
+                                      float* shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float is = 1.0f / sqrtf(rvar[c] + eps);
+    const float sc = gamma[c] * is;
+    mean[c] = rmean[c]; invstd[c] = is; scale[c] = sc; shift[c] = beta[c] - rmean[c] * sc;
+}
+
+// GroupNorm: block per image n; partials slab[n][nchunks][R][C].
+__global__ void gn_fwd_finalize_kernel(const float* slab, int nchunks, int R, int C, int G, double count,
+                                       const float* gamma, const float* beta, float eps, float* mean,
+                                       float* invstd, float* scale, float* shift) {
+    const int n = blockIdx.x;
+    const int cpg = C / G;
+    __shared__ float sm[64], si[64];
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        double s = 0.0, q = 0.0;
+        for (int k = 0; k < nchunks; ++k)
+            for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+                s += slab[(((long long)n * nchunks + k) * R + 0) * C + c];
+                q += slab[(((long long)n * nchunks + k) * R + 1) * C + c];
+            }
+        const double mu = s / count;
+        double var = q / count - mu * mu;
+        if (var < 0.0) var = 0.0;
+        sm[g] = (float)mu; si[g] = (float)(1.0 / sqrt(var + (double)eps));
+        mean[n * G + g] = sm[g]; invstd[n * G + g] = si[g];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const int g = c / cpg;
+        const float sc = gamma[c] * si[g];
+        scale[n * C + c] = sc; shift[n * C + c] = beta[c] - sm[g] * sc;
+    }
+}
+
+// BatchNorm backward: dgamma/dbeta (assign), dy = A*gpre + B + Cc*xhat coefficients, conv bias grad.
+__global__ void bn_bwd_finalize_kernel(const float* slab, int ntiles, int C, double count, const float* gamma,
+                                       const float* invstd, float* dgamma, float* dbeta, float* A, float* B,
+                                       float* Cc, float* dbias) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s1 = 0.0, s2 = 0.0, s5 = 0.0;
+    for (int t = 0; t < ntiles; ++t) {
+        const float* p = slab + (long long)t * 5 * C;
+        s1 += p[0 * C + c]; s2 += p[1 * C + c]; s5 += p[4 * C + c];
+    }
+    const double a = (double)gamma[c] * (double)invstd[c];
+    const double b = -a * s1 / count, cc = -a * s2 / count;
+    dgamma[c] = (float)s2; dbeta[c] = (float)s1;
+    A[c] = (float)a; B[c] = (float)b; Cc[c] = (float)cc;
+    if (dbias) dbias[c] = (float)(a * s1 + b * count + cc * s5);
+}
+
+// GroupNorm backward: block per image n. Writes per-(n,c) coefficients and per-(n,c) parameter
+// partials pdg/pdb/pdbias[n][c] (summed over n by a follow-up column reduction) and FiLM sums.
+__global__ void gn_bwd_finalize_kernel(const float* slab, int nchunks, int C, int G, double count_g, int HW,
+                                       const float* gamma, const float* invstd, float* A, float* B, float* Cc,
+                                       float* pdg, float* pdb, float* pdbias) {
+    const int n = blockIdx.x, cpg = C / G;
+    __shared__ double sdx[64], sdxx[64];
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        double a1 = 0.0, a2 = 0.0;
+        for (int k = 0; k < nchunks; ++k) {
+            const float* p = slab + ((long long)n * nchunks + k) * 5 * C;
+            for (int c = g * cpg; c < (g + 1) * cpg; ++c) { a1 += (double)gamma[c] * p[c]; a2 += (double)gamma[c] * p[C + c]; }
+        }
+        sdx[g] = a1; sdxx[g] = a2;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const int g = c / cpg;
+        double s1 = 0.0, s2 = 0.0, s5 = 0.0;
+        for (int k = 0; k < nchunks; ++k) {
+            const float* p = slab + ((long long)n * nchunks + k) * 5 * C;
+            s1 += p[c]; s2 += p[C + c]; s5 += p[4 * C + c];
+        }
+        const double is = invstd[n * G + g];
+        const double a = (double)gamma[c] * is, b = -is * sdx[g] / count_g, cc = -is * sdxx[g] / count_g;
+        A[n * C + c] = (float)a; B[n * C + c] = (float)b; Cc[n * C + c] = (float)cc;
+        pdg[n * C + c] = (float)s2; pdb[n * C + c] = (float)s1;
+        pdbias[n * C + c] = (float)(a * s1 + b * (double)HW + cc * s5);
+    }
+}
+
+// out[n][c] = sum over chunks of slab[n][k][r][c]   (FiLM dcemb / dtemb, per-sample sums)
+__global__ void slab_sum_nc_kernel(const float* slab, int N, int nchunks, int R, int r, int C, float* out) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= N * C) return;
+    const int n = idx / C, c = idx - n * C;
+    double s = 0.0;
+    for (int k = 0; k < nchunks; ++k) s += slab[(((long long)n * nchunks + k) * R + r) * C + c];
+    out[idx] = (float)s;
+}
+
+// out[c] (+)= sum_n in[n][c]
+__global__ void col_sum_kernel(const float* in, int N, int C, float* out, int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0;
+    for (int n = 0; n < N; ++n) s += in[(long long)n * C + c];
+    out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+// -------------------------------------------------------------------------------------------------
+// elementwise forward apply:  out = [pool]( [film]( relu(y*s+t) ) [+ resid] )
+// -------------------------------------------------------------------------------------------------
+template <bool POOL, bool FILM, bool RESID, bool RELU>
+__global__ __launch_bounds__(256) void norm_apply_fwd_kernel(const float* y, int ldy, int N, int H, int W, int C,
+                                                             NormP np, FilmP fp, ResidP rp, float* out, int ldo) {
+    const int C4 = C >> 2;
+    const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
+    const long long total = (long long)N * Ho * Wo * C4;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int c4 = (int)(idx % C4) * 4;
+        const long long pix = idx / C4;                  // n*Ho*Wo + p
+        const int n = (int)(pix / (Ho * Wo));
+        const int p = (int)(pix - (long long)n * Ho * Wo);
+        float o[4];
+        if constexpr (POOL) {
+            const int ho = p / Wo, wo = p - ho * Wo;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = -INFINITY;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float4 v = ld4(y + ((long long)(n * H + 2 * ho + (e >> 1)) * W + 2 * wo + (e & 1)) * ldy + c4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float z = f4get(v, j) * np.s[n * np.sn + c4 + j] + np.t[n * np.sn + c4 + j];
+                    if (RELU) z = fmaxf(z, 0.f);
+                    if (z > o[j] || isnan(z)) o[j] = z;
+                }
+            }
+        } else {
+            const float4 v = ld4(y + pix * ldy + c4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = c4 + j;
+                float z = f4get(v, j) * np.s[n * np.sn + c] + np.t[n * np.sn + c];
+                if (RELU) z = fmaxf(z, 0.f);
+                if constexpr (FILM) z = fp.a[n * fp.an + c] * z + fp.b[n * fp.bn + c];
+                if constexpr (RESID) {
+                    const int sel = n >= rp.split ? C : 0;
+                    z = rp.w[sel + c] * rp.x[pix] + rp.b[sel + c] + z;
+                }
+                o[j] = z;
+            }
+        }
+        st4(out + pix * ldo + c4, make_float4(o[0], o[1], o[2], o[3]));
+    }
+}
+
+// elementwise backward apply: dy = A*g_pre + B + Cc*xhat   (full grid; pooled / FiLM'd g_out recomputed)
+template <bool POOL, bool FILM>
+__global__ __launch_bounds__(256) void norm_apply_bwd_kernel(const float* g, int ldg, const float* y, int ldy, int N,
+                                                             int H, int W, int C, NormP np, FilmP fp, const float* A,
+                                                             const float* B, const float* Cc, int cn, float* dy,
+                                                             int lddy) {
+    const int C4 = C >> 2;
+    const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
+    const long long total = (long long)N * Ho * Wo * C4;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int c4 = (int)(idx % C4) * 4;
+        const long long pix = idx / C4;
+        const int n = (int)(pix / (Ho * Wo));
+        const int p = (int)(pix - (long long)n * Ho * Wo);
+        const float4 gv = ld4(g + pix * ldg + c4);
+        if constexpr (POOL) {
+            const int ho = p / Wo, wo = p - ho * Wo;
+            float4 yv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                yv[e] = ld4(y + ((long long)(n * H + 2 * ho + (e >> 1)) * W + 2 * wo + (e & 1)) * ldy + c4);
+            float out[4][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = c4 + j;
+                float zp[4], xh[4], best = -INFINITY; int arg = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    norm_elem(np, n, c, f4get(yv[e], j), zp[e], xh[e]);
+                    const float z = fmaxf(zp[e], 0.f);
+                    if (z > best || isnan(z)) { best = z; arg = e; }
+                }
+                const float a = A[n * cn + c], b = B[n * cn + c], cc = Cc[n * cn + c];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float gpre = (e == arg && zp[e] > 0.f) ? f4get(gv, j) : 0.f;
+                    out[e][j] = a * gpre + b + cc * xh[e];
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                st4(dy + ((long long)(n * H + 2 * ho + (e >> 1)) * W + 2 * wo + (e & 1)) * lddy + c4,
+                    make_float4(out[e][0], out[e][1], out[e][2], out[e][3]));
+        } else {
+            const float4 yv = ld4(y + pix * ldy + c4);
+            float out[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = c4 + j;
+                float zp, xh; norm_elem(np, n, c, f4get(yv, j), zp, xh);
+                float gz = f4get(gv, j);
+                if constexpr (FILM) gz *= fp.a[n * fp.an + c];
+                const float gpre = zp > 0.f ? gz : 0.f;
+                out[j] = A[n * cn + c] * gpre + B[n * cn + c] + Cc[n * cn + c] * xh;
+            }
+            st4(dy + pix * lddy + c4, make_float4(out[0], out[1], out[2], out[3]));
+        }
+    }
+}
+
+static inline int ew_blocks(long long total) {
+    long long b = (total + 255) / 256;
+    if (b > 8192) b = 8192;
+    if (b < 1) b = 1;
+    return (int)b;
+}
+
+}  // namespace cdm
+
+using namespace cdm;
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------ C ABI ------------------------------------------------
+CDM_API int cdm_reduce_stats(const float* y, int ldy, int N, int HW, int C, int csize, float* slab, void* stream) {
+    return launch_reduce(StatsF{y, ldy, HW}, N, HW, C, csize, slab, S(stream));
+}
+
+CDM_API int cdm_reduce_sum(const float* g, int ldg, int N, int HW, int C, int csize, float* slab, void* stream) {
+    return launch_reduce(SumF{g, ldg, HW}, N, HW, C, csize, slab, S(stream));
+}
+
+// mode: 0 plain, 1 pooled g (2x2 max pool after the relu), 2 FiLM after the relu
+CDM_API int cdm_norm_bwd_reduce(int mode, const float* g, int ldg, const float* y, int ldy, int N, int H, int W, int C,
+                                const float* s, const float* t, int sn, const float* mean, const float* invstd, int mn,
+                                int cpg, const float* film_a, int film_an, int csize, float* slab, void* stream) {
+    NormP np{s, t, sn, mean, invstd, mn, cpg};
+    FilmP fp{film_a, film_an, nullptr, 0};
+    if (mode == 1)
+        return launch_reduce(NormBwdF<true, false>{g, ldg, y, ldy, H, W, np, fp}, N, (H / 2) * (W / 2), C, csize, slab,
+                             S(stream));
+    if (mode == 2)
+        return launch_reduce(NormBwdF<false, true>{g, ldg, y, ldy, H, W, np, fp}, N, H * W, C, csize, slab, S(stream));
+    return launch_reduce(NormBwdF<false, false>{g, ldg, y, ldy, H, W, np, fp}, N, H * W, C, csize, slab, S(stream));
+}
+
+CDM_API int cdm_bn_fwd_finalize(const float* slab, int ntiles, int R, int C, double count, const float* gamma,
+                                const float* beta, float* rmean, float* rvar, long long* nbt, float momentum, float eps,
+                                float* mean, float* invstd, float* scale, float* shift, void* stream) {
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), slab, ntiles, R, C, count,
+                       gamma, beta, rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift);
+    return cdm_status();
+}
+
+CDM_API int cdm_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                               float eps, float* mean, float* invstd, float* scale, float* shift, void* stream) {
+    hipLaunchKernelGGL(bn_eval_coeffs_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), C, gamma, beta, rmean, rvar,
+                       eps, mean, invstd, scale, shift);
+    return cdm_status();
+}
+
+CDM_API int cdm_gn_fwd_finalize(const float* slab, int N, int nchunks, int R, int C, int G, double count,
+                                const float* gamma, const float* beta, float eps, float* mean, float* invstd,
+                                float* scale, float* shift, void* stream) {
+    if (G > 64) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(gn_fwd_finalize_kernel, dim3(N), dim3(256), 0, S(stream), slab, nchunks, R, C, G, count, gamma,
+                       beta, eps, mean, invstd, scale, shift);
+    return cdm_status();
+}
+
+CDM_API int cdm_bn_bwd_finalize(const float* slab, int ntiles, int C, double count, const float* gamma,
+                                const float* invstd, float* dgamma, float* dbeta, float* A, float* B, float* Cc,
+                                float* dbias, void* stream) {
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), slab, ntiles, C, count,
+                       gamma, invstd, dgamma, dbeta, A, B, Cc, dbias);
+    return cdm_status();
+}
+
+CDM_API int cdm_gn_bwd_finalize(const float* slab, int N, int nchunks, int C, int G, double count_g, int HW,
+                                const float* gamma, const float* invstd, float* A, float* B, float* Cc, float* pdg,
+                                float* pdb, float* pdbias, void* stream) {
+    if (G > 64) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(N), dim3(256), 0, S(stream), slab, nchunks, C, G, count_g, HW, gamma,
+                       invstd, A, B, Cc, pdg, pdb, pdbias);
+    return cdm_status();
+}
+
+CDM_API int cdm_slab_sum_nc(const float* slab, int N, int nchunks, int R, int r, int C, float* out, void* stream) {
+    hipLaunchKernelGGL(slab_sum_nc_kernel, dim3((N * C + 255) / 256), dim3(256), 0, S(stream), slab, N, nchunks, R, r, C,
+                       out);
+    return cdm_status();
+}
+
+CDM_API int cdm_col_sum(const float* in, int N, int C, float* out, int accumulate, void* stream) {
+    hipLaunchKernelGGL(col_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), in, N, C, out, accumulate);
+    return cdm_status();
+}
+
+// flags: 1 pool, 2 film, 4 resid, 8 relu
+CDM_API int cdm_norm_apply_fwd(int flags, const float* y, int ldy, int N, int H, int W, int C, const float* s,
+                               const float* t, int sn, const float* film_a, int film_an, const float* film_b,
+                               int film_bn, const float* rx, const float* rw, const float* rb, int rsplit, float* out,
+                               int ldo, void* stream) {
+    if (C % 4) return (int)hipErrorInvalidValue;
+    NormP np{s, t, sn, nullptr, nullptr, 0, 1};
+    FilmP fp{film_a, film_an, film_b, film_bn};
+    ResidP rp{rx, rw, rb, rsplit};
+    const bool pool = flags & 1, film = flags & 2, resid = flags & 4, relu = flags & 8;
+    const long long total = (long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 4);
+    const int nb = ew_blocks(total);
+#define CDM_APPLY(P, F, Rz, Rl) \
+    hipLaunchKernelGGL((norm_apply_fwd_kernel<P, F, Rz, Rl>), dim3(nb), dim3(256), 0, S(stream), y, ldy, N, H, W, C, np, fp, rp, out, ldo)
+    if (pool) {
+        if (film || resid) return (int)hipErrorInvalidValue;
+        if (relu) CDM_APPLY(true, false, false, true); else CDM_APPLY(true, false, false, false);
+    } else if (film) {
+        if (resid) return (int)hipErrorInvalidValue;
+        if (relu) CDM_APPLY(false, true, false, true); else CDM_APPLY(false, true, false, false);
+    } else if (resid) {
+        if (relu) CDM_APPLY(false, false, true, true); else CDM_APPLY(false, false, true, false);
+    } else {
+        if (relu) CDM_APPLY(false, false, false, true); else CDM_APPLY(false, false, false, false);
+    }
+#undef CDM_APPLY
+    return cdm_status();
+}
+
+CDM_API int cdm_norm_apply_bwd(int mode, const float* g, int ldg, const float* y, int ldy, int N, int H, int W, int C,
+                               const float* s, const float* t, int sn, const float* mean, const float* invstd, int mn,
+                               int cpg, const float* film_a, int film_an, const float* A, const float* B,
+                               const float* Cc, int cn, float* dy, int lddy, void* stream) {
+    if (C % 4) return (int)hipErrorInvalidValue;
+    NormP np{s, t, sn, mean, invstd, mn, cpg};
+    FilmP fp{film_a, film_an, nullptr, 0};
+    const long long total = (long long)N * (mode == 1 ? (H / 2) * (W / 2) : H * W) * (C / 4);
+    const int nb = ew_blocks(total);
+    if (mode == 1)
+        hipLaunchKernelGGL((norm_apply_bwd_kernel<true, false>), dim3(nb), dim3(256), 0, S(stream), g, ldg, y, ldy, N, H, W,
+                           C, np, fp, A, B, Cc, cn, dy, lddy);
+    else if (mode == 2)
+        hipLaunchKernelGGL((norm_apply_bwd_kernel<false, true>), dim3(nb), dim3(256), 0, S(stream), g, ldg, y, ldy, N, H,
+                           W, C, np, fp, A, B, Cc, cn, dy, lddy);
+    else
+        hipLaunchKernelGGL((norm_apply_bwd_kernel<false, false>), dim3(nb), dim3(256), 0, S(stream), g, ldg, y, ldy, N, H,
+                           W, C, np, fp, A, B, Cc, cn, dy, lddy);
+    return cdm_status();
+}

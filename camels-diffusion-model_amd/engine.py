@@ -1,0 +1,616 @@
+"""ContextUnet forward / backward on the HIP kernels (explicit graph, no autograd inside).
+
+Mirrors ContextUnet.forward (ContextUnet.py:42-60, == code/train_diffusion.py:48-66) block by block:
+
+    init_conv (ResidualConvBlock is_res, random 1x1 shortcut)   diffusion_utilities.py:13-65
+    down1/down2 (2x RCB + MaxPool2d(2))                          diffusion_utilities.py:103-116
+    to_vec (AvgPool2d(h/4) + GELU)                               ContextUnet.py:17
+    4x EmbedFC                                                    diffusion_utilities.py:118-145
+    up0 (ConvTranspose2d k=h/4 on 1x1, GroupNorm(8), ReLU)       ContextUnet.py:26-30
+    FiLM cemb*u + temb, up1/up2 (cat, ConvT 2x2, 2x RCB)         ContextUnet.py:57-58, diffusion_utilities.py:79-100
+    out (conv3x3, GroupNorm(8), ReLU, conv3x3 -> 1)              ContextUnet.py:35-40
+
+Memory layout: every activation is NHWC fp32 in HBM.  The three torch.cat calls are eliminated by
+giving each concatenation a single buffer whose channel slices are written by their producers:
+
+    catO  [B, H,   H,   2nf] = [ up2 output | init_conv output x0 ]
+    catU2 [B, H/2, H/2, 2nf] = [ FiLM2(up1 output) | d1 = down1 output ]
+    catU1 [B, H/4, H/4, 4nf] = [ FiLM1(up0 output) | d2 = down2 output ]
+
+Train mode keeps every BatchNorm's pre-norm conv output y (the normalised/ReLU'd activation z is
+kept only where the next conv reads it); the backward recomputes relu masks / max-pool argmaxes /
+x-hat from y.  Eval mode folds BatchNorm into the conv weights and runs ReLU in the conv epilogue.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import torch
+
+from ._lib import Mlp4, MlpDesc, lib
+
+BN_EPS = 1e-5
+BN_MOM = 0.1
+GN_EPS = 1e-5
+GN_GROUPS = 8
+CHUNK = 128           # pixels per statistics partial (== GEMM M tile)
+EPI_RELU, EPI_ACCUM = 1, 2
+APPLY_POOL, APPLY_FILM, APPLY_RESID, APPLY_RELU = 1, 2, 4, 8
+
+
+def _p(t: Optional[torch.Tensor], off: int = 0):
+    return None if t is None else t.data_ptr() + 4 * off
+
+
+class Act:
+    """NHWC activation view: channels [off, off+C) of a buffer whose pixel stride is ``ld`` floats."""
+    __slots__ = ("buf", "C", "ld", "off")
+
+    def __init__(self, buf: torch.Tensor, C: int, ld: Optional[int] = None, off: int = 0):
+        self.buf, self.C, self.ld, self.off = buf, C, (C if ld is None else ld), off
+
+    @property
+    def p(self):
+        return self.buf.data_ptr() + 4 * self.off
+
+    def sl(self, c0: int, C: int) -> "Act":
+        return Act(self.buf, C, self.ld, self.off + c0)
+
+
+def _cdiv(a, b):
+    return (a + b - 1) // b
+
+
+class LayerSpec:
+    """One Conv3x3 -> BatchNorm2d -> ReLU (diffusion_utilities.py:26-37)."""
+
+    def __init__(self, name, cin, cout, S):
+        self.name, self.cin, self.cout, self.S = name, cin, cout, S
+        self.w, self.b = name + ".0.weight", name + ".0.bias"
+        self.bn = name + ".1"
+
+
+def conv_layers(nf: int, H: int):
+    L = []
+
+    def rcb(prefix, cin, cout, S):
+        L.append(LayerSpec(prefix + ".conv1", cin, cout, S))
+        L.append(LayerSpec(prefix + ".conv2", cout, cout, S))
+
+    rcb("init_conv", 1, nf, H)
+    rcb("down1.model.0", nf, nf, H); rcb("down1.model.1", nf, nf, H)
+    rcb("down2.model.0", nf, 2 * nf, H // 2); rcb("down2.model.1", 2 * nf, 2 * nf, H // 2)
+    rcb("up1.model.1", nf, nf, H // 2); rcb("up1.model.2", nf, nf, H // 2)
+    rcb("up2.model.1", nf, nf, H); rcb("up2.model.2", nf, nf, H)
+    return L
+
+
+MLPS = ("contextembed1", "timeembed1", "contextembed2", "timeembed2")
+
+
+class UNetEngine:
+    """Kernel-level ContextUnet for one (n_feat, n_cfeat, height) on one device."""
+
+    def __init__(self, n_feat: int, n_cfeat: int, height: int, device):
+        if n_feat % 8 or height % 16:
+            raise ValueError("HIP path needs n_feat % 8 == 0 and height % 16 == 0")
+        self.nf, self.ncf, self.H = n_feat, n_cfeat, height
+        self.device = torch.device(device)
+        self.layers = conv_layers(n_feat, height)
+        self.L = {l.name: l for l in self.layers}
+        self.KK0 = (height // 4) ** 2
+        self.pk: Dict[str, torch.Tensor] = {}
+        self._pk_key = None
+        self._ones = torch.ones(4 * n_feat, device=self.device)
+        self._zeros = torch.zeros(4 * n_feat, device=self.device)
+
+    # ------------------------------------------------------------------------------------------
+    # weight packing (OIHW / [Cin][Cout][kh][kw] -> GEMM layouts; eval: BatchNorm folded)
+    # ------------------------------------------------------------------------------------------
+    def repack(self, P: Dict[str, torch.Tensor], train: bool, stream: int, key=None):
+        if key is not None and self._pk_key == (key, train):
+            return
+        lb = lib(); nf = self.nf
+        for l in self.layers:
+            W, b = P[l.w], P[l.b]
+            if train:
+                wpk = self._buf(l.name + ".wpk", (9 * l.cin, l.cout))
+                wdg = (self._buf(l.name + ".wdg", (9 * l.cout, l.cin))) if l.cin > 1 else None
+                lb.cdm_pack_conv3x3(_p(W), _p(b), l.cin, l.cout, None, None, None, None, 0.0, _p(wpk), None,
+                                    _p(wdg), stream)
+                self.pk[l.name + ".wpk"] = wpk
+                if wdg is not None:
+                    self.pk[l.name + ".wdg"] = wdg
+            else:
+                wpk = self._buf(l.name + ".wpk_e", (9 * l.cin, l.cout))
+                bpk = self._buf(l.name + ".bpk_e", (l.cout))
+                bn = l.bn
+                lb.cdm_pack_conv3x3(_p(W), _p(b), l.cin, l.cout, _p(P[bn + ".weight"]), _p(P[bn + ".bias"]),
+                                    _p(P[bn + ".running_mean"]), _p(P[bn + ".running_var"]), BN_EPS, _p(wpk),
+                                    _p(bpk), None, stream)
+                self.pk[l.name + ".wpk_e"] = wpk
+                self.pk[l.name + ".bpk_e"] = bpk
+        # out.0 (GroupNorm follows: never folded)
+        wpk = self._buf("out.0.wpk", (9 * 2 * nf, nf))
+        wdg = self._buf("out.0.wdg", (9 * nf, 2 * nf))
+        lb.cdm_pack_conv3x3(_p(P["out.0.weight"]), _p(P["out.0.bias"]), 2 * nf, nf, None, None, None, None, 0.0,
+                            _p(wpk), None, _p(wdg) if train else None, stream)
+        self.pk["out.0.wpk"], self.pk["out.0.wdg"] = wpk, wdg
+        for name, cin in (("up1.model.0", 4 * nf), ("up2.model.0", 2 * nf)):
+            wt = self._buf(name + ".wt", (cin, 4 * nf))
+            wtT = self._buf(name + ".wtT", (4 * nf, cin))
+            lb.cdm_pack_convT(_p(P[name + ".weight"]), cin, nf, 4, _p(wt), _p(wtT) if train else None, stream)
+            self.pk[name + ".wt"], self.pk[name + ".wtT"] = wt, wtT
+        c0 = 2 * nf
+        w0 = self._buf("up0.wt", (c0, self.KK0 * c0))
+        w0T = self._buf("up0.wtT", (self.KK0 * c0, c0))
+        lb.cdm_pack_convT(_p(P["up0.0.weight"]), c0, c0, self.KK0, _p(w0), _p(w0T) if train else None, stream)
+        self.pk["up0.wt"], self.pk["up0.wtT"] = w0, w0T
+        for m in MLPS:
+            w2 = P[m + ".model.2.weight"]
+            E = w2.shape[0]
+            w2t = self._buf(m + ".w2t", (E, E))
+            lb.cdm_transpose(_p(w2), E, E, _p(w2t), stream)
+            self.pk[m + ".w2t"] = w2t
+        self._pk_key = (key, train) if key is not None else None
+
+    def _buf(self, name, shape):
+        shape = (shape,) if isinstance(shape, int) else tuple(shape)
+        t = self.pk.get(name)
+        if t is None or tuple(t.shape) != tuple(shape):
+            t = torch.empty(*shape, device=self.device, dtype=torch.float32)
+        return t
+
+    # ------------------------------------------------------------------------------------------
+    def workspace(self, B: int, train: bool) -> "Workspace":
+        return Workspace(self, B, train)
+
+    # ------------------------------------------------------------------------------------------
+    # forward
+    # ------------------------------------------------------------------------------------------
+    def forward(self, ws: "Workspace", P, x: torch.Tensor, t_in: torch.Tensor, c_in: Optional[torch.Tensor],
+                sc_w: torch.Tensor, sc_b: torch.Tensor, sc_split: int, stream: int, out: Optional[torch.Tensor] = None):
+        """x [B,H,W] fp32 (C=1, NCHW == NHWC), t_in [rows_t] (rows 1 or B), c_in [rows_c, ncf] or None (zeros).
+
+        sc_w/sc_b: shortcut 1x1 conv weights, [2, nf] when sc_split < B (CFG halves) else [nf]-shaped.
+        Returns eps [B, H, W] (written into ``out`` when given)."""
+        lb = lib(); s = stream
+        nf, H, B = self.nf, self.H, ws.B
+        H1, H2 = H // 2, H // 4
+        train = ws.train
+        eps = out if out is not None else ws.eps
+        ws.x_in = x
+        ws.sc_pending = (sc_w, sc_b, sc_split)
+        # ---------------- encoder ----------------
+        for l in self.layers[:10]:
+            self._conv_bn_fwd(ws, P, l, s, x)
+        # ---------------- to_vec ----------------
+        d2 = ws.catU1.sl(2 * nf, 2 * nf)
+        lb.cdm_reduce_sum(d2.p, d2.ld, B, H2 * H2, 2 * nf, H2 * H2, _p(ws.hsum), s)
+        lb.cdm_avgpool_gelu_fin(_p(ws.hsum), B, 2 * nf, H2 * H2, _p(ws.hpre), _p(ws.hv), s)
+        # ---------------- embeddings ----------------
+        rows_t = t_in.numel()
+        if c_in is None:
+            c_in = ws.c_zero
+        rows_c = c_in.shape[0]
+        ws.t_rows, ws.c_rows = rows_t, rows_c
+        ws.t_x, ws.c_x = t_in, c_in
+        d = Mlp4()
+        for k, m in enumerate(MLPS):
+            is_t = m.startswith("time")
+            E = (2 if m.endswith("1") else 1) * nf
+            md = d.m[k]
+            md.x = _p(t_in if is_t else c_in); md.rows = rows_t if is_t else rows_c
+            md.in_dim = 1 if is_t else self.ncf; md.E = E
+            md.w1 = _p(P[m + ".model.0.weight"]); md.b1 = _p(P[m + ".model.0.bias"])
+            md.w2 = _p(P[m + ".model.2.weight"]); md.w2t = _p(self.pk[m + ".w2t"]); md.b2 = _p(P[m + ".model.2.bias"])
+            md.pre = _p(ws.emb_pre[m]) if train else None
+            md.h = _p(ws.emb_h[m]) if train else None
+            md.out = _p(ws.emb[m])
+        lb.cdm_embed_fwd(ctypes_addr(d), s)
+        ws._mlp = d
+        # ---------------- up0: ConvT(k=h/4) on the 1x1 map, GroupNorm(8), ReLU, FiLM1 -> catU1[:, :2nf] ----
+        c0 = 2 * nf
+        lb.cdm_gemm_f32(_p(ws.hv), c0, B, c0, _p(self.pk["up0.wt"]), self.KK0 * c0, self.KK0 * c0, _p(ws.y0),
+                        self.KK0 * c0, _p(P["up0.0.bias"]), c0, 0, 1, None, s)
+        self._gn_fwd(ws, P, "up0.1", Act(ws.y0, c0), B, H2, c0, ws.gn0, stats_from_conv=False, stream=s)
+        ce1, te1 = ws.emb["contextembed1"], ws.emb["timeembed1"]
+        u1 = ws.catU1.sl(0, c0)
+        lb.cdm_norm_apply_fwd(APPLY_FILM | APPLY_RELU, _p(ws.y0), c0, B, H2, H2, c0, _p(ws.gn0["scale"]),
+                              _p(ws.gn0["shift"]), c0, _p(ce1), c0 if rows_c > 1 else 0, _p(te1),
+                              c0 if rows_t > 1 else 0, None, None, None, 0, u1.p, u1.ld, s)
+        # ---------------- up1 ----------------
+        lb.cdm_convT2x2_fwd(ws.catU1.p, B, H2, H2, 4 * nf, 4 * nf, _p(self.pk["up1.model.0.wt"]),
+                            _p(P["up1.model.0.bias"]), _p(ws.yT1), nf, nf, s)
+        for l in self.layers[10:14]:
+            self._conv_bn_fwd(ws, P, l, s, x)
+        # ---------------- up2 ----------------
+        lb.cdm_convT2x2_fwd(ws.catU2.p, B, H1, H1, 2 * nf, 2 * nf, _p(self.pk["up2.model.0.wt"]),
+                            _p(P["up2.model.0.bias"]), _p(ws.yT2), nf, nf, s)
+        for l in self.layers[14:18]:
+            self._conv_bn_fwd(ws, P, l, s, x)
+        # ---------------- out ----------------
+        lb.cdm_conv3x3_fwd(ws.catO.p, B, H, H, 2 * nf, 2 * nf, _p(self.pk["out.0.wpk"]), _p(P["out.0.bias"]),
+                           _p(ws.yO), nf, nf, 0, _p(ws.slab), nf, s)
+        self._gn_fwd(ws, P, "out.1", Act(ws.yO, nf), B, H, nf, ws.gnO, stats_from_conv=True, stream=s)
+        lb.cdm_norm_apply_fwd(APPLY_RELU, _p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]), _p(ws.gnO["shift"]), nf,
+                              None, 0, None, 0, None, None, None, 0, _p(ws.zO), nf, s)
+        lb.cdm_conv3x3_cout1_fwd(_p(ws.zO), nf, B, H, H, nf, _p(P["out.3.weight"]), _p(P["out.3.bias"]), _p(eps), s)
+        return eps
+
+    def _conv_bn_fwd(self, ws, P, l: LayerSpec, s, x):
+        lb = lib()
+        B, S = ws.B, l.S
+        src = ws.src[l.name]
+        y = ws.y[l.name]
+        st = ws.bn[l.name]
+        npix = B * S * S
+        if ws.train:
+            if l.cin == 1:
+                lb.cdm_conv3x3_cin1_fwd(_p(x), B, S, S, _p(self.pk[l.name + ".wpk"]), _p(P[l.b]), _p(y), l.cout,
+                                        l.cout, 0, s)
+                lb.cdm_reduce_stats(_p(y), l.cout, B, S * S, l.cout, CHUNK, _p(ws.slab), s)
+                ntiles = B * _cdiv(S * S, CHUNK)
+            else:
+                lb.cdm_conv3x3_fwd(src.p, B, S, S, l.cin, src.ld, _p(self.pk[l.name + ".wpk"]), _p(P[l.b]), _p(y),
+                                   l.cout, l.cout, 0, _p(ws.slab), l.cout, s)
+                ntiles = _cdiv(npix, CHUNK)
+            bn = l.bn
+            lb.cdm_bn_fwd_finalize(_p(ws.slab), ntiles, 2, l.cout, float(npix), _p(P[bn + ".weight"]),
+                                   _p(P[bn + ".bias"]), _p(P[bn + ".running_mean"]), _p(P[bn + ".running_var"]),
+                                   _p(P[bn + ".num_batches_tracked"]), BN_MOM, BN_EPS, _p(st["mean"]),
+                                   _p(st["invstd"]), _p(st["scale"]), _p(st["shift"]), s)
+            scale, shift, relu = st["scale"], st["shift"], APPLY_RELU
+        else:
+            kind = ws.dst_kind[l.name]
+            dense = kind in ("dense", "plain")
+            outp = ws.dst[l.name] if dense else Act(y, l.cout)
+            if l.cin == 1:
+                lb.cdm_conv3x3_cin1_fwd(_p(x), B, S, S, _p(self.pk[l.name + ".wpk_e"]),
+                                        _p(self.pk[l.name + ".bpk_e"]), outp.p, outp.ld, l.cout, 1, s)
+            else:
+                lb.cdm_conv3x3_fwd(src.p, B, S, S, l.cin, src.ld, _p(self.pk[l.name + ".wpk_e"]),
+                                   _p(self.pk[l.name + ".bpk_e"]), outp.p, outp.ld, l.cout, EPI_RELU, None, 0, s)
+            if dense:
+                return
+            scale, shift, relu = self._ones, self._zeros, 0
+        # apply: z = relu(bn(y)) -> destination (dense / pool / film / resid)
+        kind = ws.dst_kind[l.name]
+        dst = ws.dst[l.name]
+        C = l.cout
+        if kind == "dense" or kind == "plain":
+            lb.cdm_norm_apply_fwd(relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), 0, None, 0, None, 0, None, None,
+                                  None, 0, dst.p, dst.ld, s)
+        elif kind == "pool":
+            lb.cdm_norm_apply_fwd(APPLY_POOL | relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), 0, None, 0, None, 0,
+                                  None, None, None, 0, dst.p, dst.ld, s)
+        elif kind == "film":
+            ce, te = ws.emb["contextembed2"], ws.emb["timeembed2"]
+            lb.cdm_norm_apply_fwd(APPLY_FILM | relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), 0, _p(ce),
+                                  C if ws.c_rows > 1 else 0, _p(te), C if ws.t_rows > 1 else 0, None, None, None, 0,
+                                  dst.p, dst.ld, s)
+        elif kind == "resid":
+            sc_w, sc_b, split = ws.sc_pending
+            lb.cdm_norm_apply_fwd(APPLY_RESID | relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), 0, None, 0, None,
+                                  0, _p(x), _p(sc_w), _p(sc_b), split, dst.p, dst.ld, s)
+        else:
+            raise AssertionError(kind)
+
+    def _gn_fwd(self, ws, P, name, y: Act, B, S, C, st, stats_from_conv, stream):
+        lb = lib()
+        nchunks = _cdiv(S * S, CHUNK)
+        if not stats_from_conv:
+            lb.cdm_reduce_stats(y.p, y.ld, B, S * S, C, CHUNK, _p(ws.slab), stream)
+        cpg = C // GN_GROUPS
+        lb.cdm_gn_fwd_finalize(_p(ws.slab), B, nchunks, 2, C, GN_GROUPS, float(S * S * cpg), _p(P[name + ".weight"]),
+                               _p(P[name + ".bias"]), GN_EPS, _p(st["mean"]), _p(st["invstd"]), _p(st["scale"]),
+                               _p(st["shift"]), stream)
+
+    # ------------------------------------------------------------------------------------------
+    # backward (train mode workspaces only)
+    # ------------------------------------------------------------------------------------------
+    def backward(self, ws: "Workspace", P, deps: torch.Tensor, G: Dict[str, torch.Tensor], stream: int,
+                 dbias_out3: Optional[torch.Tensor] = None):
+        """deps [B,H,W] = dL/d eps.  Writes (assigns) every parameter gradient into G[name]."""
+        assert ws.train, "backward needs a train-mode workspace"
+        lb = lib(); s = stream
+        nf, H, B = self.nf, self.H, ws.B
+        H1, H2 = H // 2, H // 4
+        P0, P1, P2 = B * H * H, B * H1 * H1, B * H2 * H2
+        # ---------------- out.3 (nf -> 1) ----------------
+        nch = _cdiv(H * H, CHUNK)
+        lb.cdm_conv3x3_cout1_wgrad(_p(deps), _p(ws.zO), nf, B, H, H, nf, CHUNK, _p(ws.slab), s)
+        lb.cdm_slab_sum_all(_p(ws.slab), B * nch, 9, 0, 9, nf, _p(G["out.3.weight"]), 1, 9, 0, s)
+        if dbias_out3 is None:
+            _sum_into(deps, G["out.3.bias"], ws.slab, s)
+        else:
+            G["out.3.bias"].copy_(dbias_out3.view_as(G["out.3.bias"]))
+        gO = ws.G0
+        lb.cdm_conv3x3_cout1_dgrad(_p(deps), B, H, H, nf, _p(P["out.3.weight"]), _p(gO), nf, s)
+        # ---------------- out.1 GroupNorm + ReLU ----------------
+        dyO = ws.D0
+        self._gn_bwd(ws, P, "out.1", "out.0.bias", Act(gO, nf), 0, Act(ws.yO, nf), B, H, nf, ws.gnO, None, 0,
+                     Act(dyO, nf), G, s)
+        # ---------------- out.0 conv (2nf -> nf) ----------------
+        self._wgrad3x3(ws, Act(dyO, nf), ws.catO, B, H, 2 * nf, nf, G["out.0.weight"], s)
+        lb.cdm_conv3x3_fwd(_p(dyO), B, H, H, nf, nf, _p(self.pk["out.0.wdg"]), None, ws.dcatO.p, ws.dcatO.ld,
+                           2 * nf, 0, None, 0, s)
+        # ---------------- up2 blocks ----------------
+        self._chain_bwd(ws, P, self.layers[14:18], G, s)
+        # convT2 (2nf@H1 -> nf@H): grad wrt its output sits in ws.gT2
+        self._convT_bwd(ws, P, "up2.model.0", Act(ws.gT2, nf), ws.catU2, B, H1, 2 * nf, nf, ws.dcatU2, G, s)
+        # ---------------- up1 blocks (last one carries FiLM2) ----------------
+        self._chain_bwd(ws, P, self.layers[10:14], G, s)
+        self._convT_bwd(ws, P, "up1.model.0", Act(ws.gT1, nf), ws.catU1, B, H2, 4 * nf, nf, ws.dcatU1, G, s)
+        # ---------------- up0: GroupNorm + ReLU + FiLM1 ----------------
+        c0 = 2 * nf
+        rows_c, rows_t = ws.c_rows, ws.t_rows
+        self._gn_bwd(ws, P, "up0.1", "up0.0.bias", ws.dcatU1.sl(0, c0), 2, Act(ws.y0, c0), B, H2, c0, ws.gn0,
+                     ws.emb["contextembed1"], c0 if rows_c > 1 else 0, Act(ws.D2, c0), G, s,
+                     film_out=(ws.d_emb["contextembed1"], ws.d_emb["timeembed1"]))
+        # up0 weight: dW[ci][(ij,co)] = sum_n hv[n][ci] dy0[n][(ij,co)]  -> [ci][co][ij]
+        KN = self.KK0 * c0
+        sp = lb.raw("cdm_gemm_splits")(B, 1)
+        lb.cdm_gemm_tn_f32(_p(ws.hv), c0, c0, B, _p(ws.D2), KN, KN, 1, _p(ws.slab), s)
+        lb.cdm_slab_reduce(_p(ws.slab), sp, c0, KN, _p(G["up0.0.weight"]), KN, 1, self.KK0, c0, 0, 1.0, s)
+        # dhv[n][ci] = sum_{(ij,co)} dy0[n][(ij,co)] W[ci][co][ij]   (split-K over 16*16*2nf)
+        want = max(1, min(64, _cdiv(1024, _cdiv(B, 128) * _cdiv(c0, 128))))
+        sp = lb.raw("cdm_gemm_splits")(KN, want)
+        lb.cdm_gemm_f32(_p(ws.D2), KN, B, KN, _p(self.pk["up0.wtT"]), c0, c0, _p(ws.dhv), c0, None, 1, 0, sp,
+                        _p(ws.slab), s)
+        if sp > 1:
+            lb.cdm_slab_reduce(_p(ws.slab), sp, B, c0, _p(ws.dhv), c0, 0, 1, c0, 0, 1.0, s)
+        # to_vec: d2 grad += dhv * gelu'(hpre) / (h/4)^2
+        d2g = ws.dcatU1.sl(2 * nf, 2 * nf)
+        lb.cdm_avgpool_gelu_bwd(_p(ws.dhv), _p(ws.hpre), B, H2 * H2, c0, d2g.p, d2g.ld, s)
+        # ---------------- embeddings ----------------
+        d = ws._mlp
+        for k, m in enumerate(MLPS):
+            md = d.m[k]
+            md.dout = _p(ws.d_emb[m]); md.dpre = _p(ws.emb_dpre[m])
+            md.dw1 = _p(G[m + ".model.0.weight"]); md.db1 = _p(G[m + ".model.0.bias"])
+            md.dw2 = _p(G[m + ".model.2.weight"]); md.db2 = _p(G[m + ".model.2.bias"])
+        lb.cdm_embed_bwd(ctypes_addr(d), s)
+        # ---------------- down2, down1, init ----------------
+        self._chain_bwd(ws, P, self.layers[6:10], G, s)
+        self._chain_bwd(ws, P, self.layers[2:6], G, s)
+        self._chain_bwd(ws, P, self.layers[0:2], G, s)
+
+    def _chain_bwd(self, ws, P, layers, G, s):
+        for l in reversed(layers):
+            self._conv_bn_bwd(ws, P, l, G, s)
+
+    def _conv_bn_bwd(self, ws, P, l: LayerSpec, G, s):
+        lb = lib()
+        B, S, C = ws.B, l.S, l.cout
+        kind = ws.dst_kind[l.name]
+        g = ws.gout[l.name]
+        y = ws.y[l.name]
+        st = ws.bn[l.name]
+        mode = {"dense": 0, "plain": 0, "resid": 0, "pool": 1, "film": 2}[kind]
+        film_a, film_an = None, 0
+        if mode == 2:
+            film_a, film_an = ws.emb["contextembed2"], (C if ws.c_rows > 1 else 0)
+        HWp = (S // 2) * (S // 2) if mode == 1 else S * S
+        nch = _cdiv(HWp, CHUNK)
+        lb.cdm_norm_bwd_reduce(mode, g.p, g.ld, _p(y), C, B, S, S, C, _p(st["scale"]), _p(st["shift"]), 0,
+                               _p(st["mean"]), _p(st["invstd"]), 0, 1, _p(film_a), film_an, CHUNK, _p(ws.slab), s)
+        if mode == 2:  # FiLM2 sums -> d cemb2 / d temb2 (per sample)
+            lb.cdm_slab_sum_nc(_p(ws.slab), B, nch, 5, 2, C, _p(ws.d_emb["contextembed2"]), s)
+            lb.cdm_slab_sum_nc(_p(ws.slab), B, nch, 5, 3, C, _p(ws.d_emb["timeembed2"]), s)
+        co = ws.coef
+        bn = l.bn
+        lb.cdm_bn_bwd_finalize(_p(ws.slab), B * nch, C, float(B * S * S), _p(P[bn + ".weight"]), _p(st["invstd"]),
+                               _p(G[bn + ".weight"]), _p(G[bn + ".bias"]), _p(co[0]), _p(co[1]), _p(co[2]),
+                               _p(G[l.b]), s)
+        dy = ws.dy[l.name]
+        lb.cdm_norm_apply_bwd(mode, g.p, g.ld, _p(y), C, B, S, S, C, _p(st["scale"]), _p(st["shift"]), 0,
+                              _p(st["mean"]), _p(st["invstd"]), 0, 1, _p(film_a), film_an, _p(co[0]), _p(co[1]),
+                              _p(co[2]), 0, dy.p, dy.ld, s)
+        src = ws.src[l.name]
+        if l.cin == 1:
+            lb.cdm_conv3x3_cin1_wgrad(dy.p, dy.ld, _p(ws.x_in), B, S, S, C, CHUNK, _p(ws.slab), s)
+            lb.cdm_slab_sum_all(_p(ws.slab), B * _cdiv(S * S, CHUNK), 10, 0, 9, C, _p(G[l.w]), 1, 9, 0, s)
+            return
+        self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s)
+        dgd = ws.dgrad_dst[l.name]
+        lb.cdm_conv3x3_fwd(dy.p, B, S, S, C, dy.ld, _p(self.pk[l.name + ".wdg"]), None, dgd.p, dgd.ld, l.cin,
+                           EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, s)
+
+    def _wgrad3x3(self, ws, dy: Act, x: Act, B, S, cin, cout, gW, s):
+        lb = lib()
+        sp = wgrad_splits(B * S * S, cout, 9 * cin)
+        lb.cdm_conv3x3_wgrad(dy.p, dy.ld, cout, x.p, B, S, S, cin, x.ld, sp, _p(ws.slab), s)
+        # slab[z][co][tap*cin+ci] -> OIHW [co][ci][tap]
+        lb.cdm_slab_reduce(_p(ws.slab), sp, cout, 9 * cin, _p(gW), 9 * cin, 1, 9, cin, 0, 1.0, s)
+
+    def _convT_bwd(self, ws, P, name, gy: Act, x: Act, B, Hin, cin, cout, dx: Act, G, s):
+        """ConvTranspose2d(cin, cout, 2, 2) backward; gy is the grad of its output [B, 2Hin, 2Hin, cout]."""
+        lb = lib()
+        Ho = 2 * Hin
+        lb.cdm_reduce_sum(gy.p, gy.ld, B, Ho * Ho, cout, CHUNK, _p(ws.slab), s)
+        lb.cdm_slab_sum_all(_p(ws.slab), B * _cdiv(Ho * Ho, CHUNK), 1, 0, 1, cout, _p(G[name + ".bias"]), 0, 1, 0, s)
+        sp = wgrad_splits(B * Hin * Hin, cin, 4 * cout)
+        lb.cdm_convT2x2_wgrad(x.p, B, Hin, Hin, cin, x.ld, gy.p, cout, gy.ld, sp, _p(ws.slab), s)
+        # slab[z][ci][ij*cout+co] -> [ci][co][ij]
+        lb.cdm_slab_reduce(_p(ws.slab), sp, cin, 4 * cout, _p(G[name + ".weight"]), 4 * cout, 1, 4, cout, 0, 1.0, s)
+        lb.cdm_convT2x2_dgrad(gy.p, B, Hin, Hin, cout, gy.ld, _p(self.pk[name + ".wtT"]), dx.p, dx.ld, cin, 0, s)
+
+    def _gn_bwd(self, ws, P, name, bias_name, g: Act, mode, y: Act, B, S, C, st, film_a, film_an, dy: Act, G, s,
+                film_out=None):
+        lb = lib()
+        nch = _cdiv(S * S, CHUNK)
+        cpg = C // GN_GROUPS
+        lb.cdm_norm_bwd_reduce(mode, g.p, g.ld, y.p, y.ld, B, S, S, C, _p(st["scale"]), _p(st["shift"]), C,
+                               _p(st["mean"]), _p(st["invstd"]), GN_GROUPS, cpg, _p(film_a), film_an, CHUNK,
+                               _p(ws.slab), s)
+        if film_out is not None:
+            lb.cdm_slab_sum_nc(_p(ws.slab), B, nch, 5, 2, C, _p(film_out[0]), s)
+            lb.cdm_slab_sum_nc(_p(ws.slab), B, nch, 5, 3, C, _p(film_out[1]), s)
+        co = ws.gcoef
+        lb.cdm_gn_bwd_finalize(_p(ws.slab), B, nch, C, GN_GROUPS, float(S * S * cpg), S * S, _p(P[name + ".weight"]),
+                               _p(st["invstd"]), _p(co[0]), _p(co[1]), _p(co[2]), _p(co[3]), _p(co[4]), _p(co[5]), s)
+        lb.cdm_col_sum(_p(co[3]), B, C, _p(G[name + ".weight"]), 0, s)
+        lb.cdm_col_sum(_p(co[4]), B, C, _p(G[name + ".bias"]), 0, s)
+        if bias_name is not None:
+            lb.cdm_col_sum(_p(co[5]), B, C, _p(G[bias_name]), 0, s)
+        lb.cdm_norm_apply_bwd(mode, g.p, g.ld, y.p, y.ld, B, S, S, C, _p(st["scale"]), _p(st["shift"]), C,
+                              _p(st["mean"]), _p(st["invstd"]), GN_GROUPS, cpg, _p(film_a), film_an, _p(co[0]),
+                              _p(co[1]), _p(co[2]), C, dy.p, dy.ld, s)
+
+
+def _sum_into(x: torch.Tensor, out: torch.Tensor, scratch: torch.Tensor, stream: int):
+    """out[0] = sum(x) for a C=1 map: C=4 column partials over a [n/4, 4] view, then fold."""
+    lb = lib()
+    n = x.numel()
+    assert n % 4 == 0
+    nch = _cdiv(n // 4, CHUNK)
+    lb.cdm_reduce_sum(_p(x), 4, 1, n // 4, 4, CHUNK, _p(scratch), stream)
+    part = scratch[4 * nch: 4 * nch + 4]
+    lb.cdm_slab_sum_all(_p(scratch), nch, 1, 0, 1, 4, _p(part), 0, 1, 0, stream)
+    lb.cdm_col_sum(_p(part), 4, 1, _p(out), 0, stream)
+
+
+def wgrad_splits(K: int, M: int, N: int) -> int:
+    """Split-K factor for a weight-gradient GEMM: aim for ~2048 workgroups."""
+    tiles = _cdiv(M, 128) * _cdiv(N, 128)
+    want = max(1, min(512, _cdiv(2048, tiles)))
+    return lib().raw("cdm_gemm_splits")(K, want)
+
+
+def ctypes_addr(obj):
+    import ctypes
+    return ctypes.addressof(obj)
+
+
+class Workspace:
+    """All device buffers for one batch size and mode (train keeps what backward needs)."""
+
+    def __init__(self, eng: UNetEngine, B: int, train: bool):
+        self.eng, self.B, self.train = eng, B, train
+        dev = eng.device
+        nf, H, ncf = eng.nf, eng.H, eng.ncf
+        H1, H2 = H // 2, H // 4
+        P0, P1, P2 = B * H * H, B * H1 * H1, B * H2 * H2
+        E = lambda *shape: torch.empty(*shape, device=dev, dtype=torch.float32)
+        self.catO = Act(E(P0, 2 * nf), 2 * nf)
+        self.catU2 = Act(E(P1, 2 * nf), 2 * nf)
+        self.catU1 = Act(E(P2, 4 * nf), 4 * nf)
+        self.eps = E(B, H, H)
+        self.yT1 = E(P1, nf)
+        self.yT2 = E(P0, nf)
+        self.y0 = E(P2, 2 * nf)
+        self.yO = E(P0, nf)
+        self.zO = E(P0, nf)
+        self.hsum, self.hpre, self.hv = E(B, 2 * nf), E(B, 2 * nf), E(B, 2 * nf)
+        self.c_zero = torch.zeros(B, ncf, device=dev)
+        self.emb = {m: E(B, (2 if m.endswith("1") else 1) * nf) for m in MLPS}
+        if train:
+            self.emb_pre = {m: E(B, (2 if m.endswith("1") else 1) * nf) for m in MLPS}
+            self.emb_h = {m: E(B, (2 if m.endswith("1") else 1) * nf) for m in MLPS}
+            self.emb_dpre = {m: E(B, (2 if m.endswith("1") else 1) * nf) for m in MLPS}
+            self.d_emb = {m: E(B, (2 if m.endswith("1") else 1) * nf) for m in MLPS}
+        self.gn0 = {k: E(B * 2 * nf) for k in ("mean", "invstd", "scale", "shift")}
+        self.gnO = {k: E(B * nf) for k in ("mean", "invstd", "scale", "shift")}
+        # per conv-BN layer: y (pre-norm), z destinations, BN coefficients
+        L = eng.layers
+        self.y, self.src, self.dst, self.dst_kind, self.bn = {}, {}, {}, {}, {}
+        z = {}
+        for l in L:
+            npx = B * l.S * l.S
+            self.y[l.name] = E(npx, l.cout)
+            self.bn[l.name] = {k: E(l.cout) for k in ("mean", "invstd", "scale", "shift")}
+        names = [l.name for l in L]
+        # destinations of each layer's activation output
+        kinds = {}
+        for i, l in enumerate(L):
+            kinds[l.name] = "dense"
+        kinds["init_conv.conv2"] = "resid"
+        kinds["down1.model.1.conv2"] = "pool"
+        kinds["down2.model.1.conv2"] = "pool"
+        kinds["up1.model.2.conv2"] = "film"
+        kinds["up2.model.2.conv2"] = "plain"
+        self.dst_kind = kinds
+        for l in L:
+            k = kinds[l.name]
+            if k == "dense":
+                z[l.name] = Act(E(B * l.S * l.S, l.cout), l.cout)
+                self.dst[l.name] = z[l.name]
+        self.dst["init_conv.conv2"] = self.catO.sl(nf, nf)
+        self.dst["down1.model.1.conv2"] = self.catU2.sl(nf, nf)
+        self.dst["down2.model.1.conv2"] = self.catU1.sl(2 * nf, 2 * nf)
+        self.dst["up1.model.2.conv2"] = self.catU2.sl(0, nf)
+        self.dst["up2.model.2.conv2"] = self.catO.sl(0, nf)
+        # inputs of each conv
+        prev = {names[i]: names[i - 1] for i in range(1, len(names))}
+        for l in L:
+            if l.name == "init_conv.conv1":
+                self.src[l.name] = None
+            elif l.name == "down1.model.0.conv1":
+                self.src[l.name] = self.catO.sl(nf, nf)
+            elif l.name == "down2.model.0.conv1":
+                self.src[l.name] = self.catU2.sl(nf, nf)
+            elif l.name == "up1.model.1.conv1":
+                self.src[l.name] = Act(self.yT1, nf)
+            elif l.name == "up2.model.1.conv1":
+                self.src[l.name] = Act(self.yT2, nf)
+            else:
+                self.src[l.name] = self.dst[prev[l.name]]
+        self.slab = E(self._slab_floats())
+        self.sc_pending = None
+        if train:
+            C4 = 4 * nf
+            self.G0, self.D0 = E(P0, 2 * nf), E(P0, 2 * nf)
+            self.G1, self.D1 = E(P1, 2 * nf), E(P1, 2 * nf)
+            self.D2 = E(P2, 4 * nf)
+            self.gT1, self.gT2 = self.G1, self.G0
+            self.dcatO = Act(E(P0, 2 * nf), 2 * nf)
+            self.dcatU2 = Act(E(P1, 2 * nf), 2 * nf)
+            self.dcatU1 = Act(E(P2, 4 * nf), 4 * nf)
+            self.dhv = E(B, 2 * nf)
+            self.coef = [E(C4) for _ in range(3)]
+            self.gcoef = [E(B * C4) for _ in range(6)]
+            # backward wiring: grad of each layer's output (gout), its dy buffer and dgrad destination
+            self.gout, self.dy, self.dgrad_dst, self.dgrad_accum = {}, {}, {}, {}
+            for l in L:
+                Gb = self.G0 if l.S == H else self.G1
+                Db = self.D0 if l.S == H else self.D1
+                self.dy[l.name] = Act(Db, l.cout)
+                k = kinds[l.name]
+                if k == "resid":
+                    self.gout[l.name] = self.dcatO.sl(nf, nf)
+                elif k == "pool":
+                    self.gout[l.name] = (self.dcatU2.sl(nf, nf) if l.name.startswith("down1")
+                                         else self.dcatU1.sl(2 * nf, 2 * nf))
+                elif k == "film":
+                    self.gout[l.name] = self.dcatU2.sl(0, nf)
+                elif k == "plain":
+                    self.gout[l.name] = self.dcatO.sl(0, nf)
+                else:
+                    self.gout[l.name] = Act(Gb, l.cout)   # written by the next layer's dgrad
+                # where this layer's dgrad (grad wrt its input) goes
+                if l.name == "down1.model.0.conv1":
+                    self.dgrad_dst[l.name], self.dgrad_accum[l.name] = self.dcatO.sl(nf, nf), True
+                elif l.name == "down2.model.0.conv1":
+                    self.dgrad_dst[l.name], self.dgrad_accum[l.name] = self.dcatU2.sl(nf, nf), True
+                elif l.name in ("up1.model.1.conv1", "up2.model.1.conv1"):
+                    self.dgrad_dst[l.name], self.dgrad_accum[l.name] = Act(Gb, l.cin), False
+                elif l.cin > 1:
+                    self.dgrad_dst[l.name], self.dgrad_accum[l.name] = Act(Gb, l.cin), False
+
+    def _slab_floats(self):
+        eng, B = self.eng, self.B
+        nf, H = eng.nf, eng.H
+        P0 = B * H * H
+        need = _cdiv(P0, CHUNK) * 10 * 2 * nf          # stats / bwd partials at full res (R <= 10)
+        if self.train:
+            for l in eng.layers:                         # conv wgrad split-K slabs
+                if l.cin > 1:
+                    sp = wgrad_splits(B * l.S * l.S, l.cout, 9 * l.cin)
+                    need = max(need, sp * l.cout * 9 * l.cin)
+            for cin, Hin in ((4 * nf, H // 4), (2 * nf, H // 2)):   # convT wgrad
+                need = max(need, wgrad_splits(B * Hin * Hin, cin, 4 * nf) * cin * 4 * nf)
+            need = max(need, 2 * nf * eng.KK0 * 2 * nf)     # up0 weight grad
+            need = max(need, 64 * B * 2 * nf)               # up0 dgrad split-K
+        return int(need)

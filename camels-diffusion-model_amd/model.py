@@ -1,0 +1,233 @@
+"""Drop-in ``ContextUnet`` (ContextUnet.py:5-60) whose forward/backward run on the HIP engine.
+
+Parameter tree, names, shapes, default initialisation order and therefore the seeded weights are
+identical to the reference, so ``state_dict()`` / ``load_state_dict()`` are interchangeable with
+checkpoints of the reference (156 entries incl. BatchNorm buffers).  The building blocks keep the
+reference constructor signatures (diffusion_utilities.py:13-145) and act as parameter holders:
+the network is executed as a whole by :class:`cdm_amd.engine.UNetEngine`.
+
+The reference draws a *fresh* random 1x1 shortcut convolution on every forward call
+(diffusion_utilities.py:54).  ``shortcut_source`` selects where that draw comes from:
+``"cpu"`` (default) consumes the CPU torch RNG exactly as the reference does (bit-compatible
+seeding), ``"device"`` draws the same U(-1, 1) distribution from on-device Philox (no host work;
+used by the captured train/sample loops).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from .engine import UNetEngine
+
+# ------------------------------------------------------------------------------------------------
+# building blocks (constructor-compatible with code/diffusion_utilities.py)
+# ------------------------------------------------------------------------------------------------
+
+
+def _conv_bn_relu(cin: int, cout: int) -> nn.Sequential:
+    return nn.Sequential(nn.Conv2d(cin, cout, 3, 1, 1), nn.BatchNorm2d(cout), nn.ReLU())
+
+
+class _Holder(nn.Module):
+    def forward(self, *a, **k):  # pragma: no cover - explicit by design
+        raise RuntimeError(f"{type(self).__name__} is executed as part of ContextUnet on the HIP engine; "
+                           "call ContextUnet.forward")
+
+
+class ResidualConvBlock(_Holder):
+    """diffusion_utilities.py:13-37 — conv1/conv2 = Conv3x3 -> BatchNorm2d -> ReLU."""
+
+    def __init__(self, in_channels: int, out_channels: int, is_res: bool = False) -> None:
+        super().__init__()
+        self.same_channels = in_channels == out_channels
+        self.is_res = is_res
+        self.conv1 = _conv_bn_relu(in_channels, out_channels)
+        self.conv2 = _conv_bn_relu(out_channels, out_channels)
+
+    def get_out_channels(self):
+        return self.conv2[0].out_channels
+
+
+class UnetUp(_Holder):
+    """diffusion_utilities.py:79-100 — ConvTranspose2d(in,out,2,2) + 2 residual-free conv blocks."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.model = nn.Sequential(nn.ConvTranspose2d(in_channels, out_channels, 2, 2),
+                                   ResidualConvBlock(out_channels, out_channels),
+                                   ResidualConvBlock(out_channels, out_channels))
+
+
+class UnetDown(_Holder):
+    """diffusion_utilities.py:103-116 — 2 conv blocks + MaxPool2d(2)."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.model = nn.Sequential(ResidualConvBlock(in_channels, out_channels),
+                                   ResidualConvBlock(out_channels, out_channels), nn.MaxPool2d(2))
+
+
+class EmbedFC(_Holder):
+    """diffusion_utilities.py:118-145 — Linear(in,e) -> GELU -> Linear(e,e)."""
+
+    def __init__(self, input_dim, emb_dim):
+        super().__init__()
+        self.input_dim = input_dim
+        self.model = nn.Sequential(nn.Linear(input_dim, emb_dim), nn.GELU(), nn.Linear(emb_dim, emb_dim))
+
+
+# ------------------------------------------------------------------------------------------------
+# engine registry / autograd bridge
+# ------------------------------------------------------------------------------------------------
+_ENGINES: Dict[tuple, UNetEngine] = {}
+
+
+def get_engine(n_feat, n_cfeat, height, device) -> UNetEngine:
+    dev = torch.device(device)
+    key = (n_feat, n_cfeat, height, dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+    eng = _ENGINES.get(key)
+    if eng is None:
+        eng = _ENGINES[key] = UNetEngine(n_feat, n_cfeat, height, dev)
+    return eng
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+class _UNetFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, holder, x, t, c, sc_w, sc_b, *params):
+        mod: "ContextUnet" = holder[0]
+        eng, P = mod._engine_and_params()
+        s = _stream()
+        B = x.shape[0]
+        eng.repack(P, True, s)
+        ws = eng.workspace(B, True)
+        eps = eng.forward(ws, P, x.reshape(B, mod.h, mod.h), t, c, sc_w, sc_b, B, s)
+        mod._invalidate_eval_pack()
+        ctx.state = (mod, eng, ws, P)
+        return eps.view(B, 1, mod.h, mod.h)
+
+    @staticmethod
+    def backward(ctx, geps):
+        mod, eng, ws, P = ctx.state
+        if ws.t_rows != ws.B or ws.c_rows != ws.B:
+            raise NotImplementedError("backward needs per-sample t and c (the reference training step's shapes)")
+        names = mod._param_names
+        G = {n: torch.empty_like(P[n]) for n in names}
+        eng.backward(ws, P, geps.reshape(ws.B, mod.h, mod.h).contiguous(), G, _stream())
+        ctx.state = None
+        return (None, None, None, None, None, None, *[G[n] for n in names])
+
+
+class ContextUnet(nn.Module):
+    """Drop-in for ContextUnet.py:5-60 (same constructor, attributes, state_dict and forward)."""
+
+    def __init__(self, in_channels, n_feat=128, n_cfeat=10, height=64, shortcut_source: str = "cpu"):
+        super().__init__()
+        self.in_channels, self.n_feat, self.n_cfeat, self.h = in_channels, n_feat, n_cfeat, height
+        # construction order == reference order, so seeded default init reproduces its weights
+        self.init_conv = ResidualConvBlock(in_channels, n_feat, is_res=True)
+        self.down1 = UnetDown(n_feat, n_feat)
+        self.down2 = UnetDown(n_feat, 2 * n_feat)
+        self.to_vec = nn.Sequential(nn.AvgPool2d(height // 4), nn.GELU())
+        self.timeembed1 = EmbedFC(1, 2 * n_feat)
+        self.timeembed2 = EmbedFC(1, n_feat)
+        self.contextembed1 = EmbedFC(n_cfeat, 2 * n_feat)
+        self.contextembed2 = EmbedFC(n_cfeat, n_feat)
+        self.up0 = nn.Sequential(nn.ConvTranspose2d(2 * n_feat, 2 * n_feat, height // 4, height // 4),
+                                 nn.GroupNorm(8, 2 * n_feat), nn.ReLU())
+        self.up1 = UnetUp(4 * n_feat, n_feat)
+        self.up2 = UnetUp(2 * n_feat, n_feat)
+        self.out = nn.Sequential(nn.Conv2d(2 * n_feat, n_feat, 3, 1, 1), nn.GroupNorm(8, n_feat), nn.ReLU(),
+                                 nn.Conv2d(n_feat, in_channels, 3, 1, 1))
+        if shortcut_source not in ("cpu", "device"):
+            raise ValueError("shortcut_source must be 'cpu' or 'device'")
+        self.shortcut_source = shortcut_source
+        self._param_names: List[str] = [n for n, _ in self.named_parameters()]
+        self._eval_key = None
+        self._sc_counter = 0
+
+    # -------------------------------------------------------------------------------------------
+    def _engine_and_params(self):
+        if self.in_channels != 1:
+            raise NotImplementedError("the HIP path implements the reference's in_channels=1 maps")
+        P = dict(self.named_parameters())
+        P.update(dict(self.named_buffers()))
+        dev = P["out.3.weight"].device
+        if dev.type != "cuda":
+            raise RuntimeError("ContextUnet runs on the MI355X HIP engine: move the module to a cuda device")
+        for k, v in P.items():
+            if k.endswith("num_batches_tracked"):
+                continue
+            if v.dtype != torch.float32 or not v.is_contiguous():
+                raise RuntimeError(f"{k}: expected contiguous fp32 (got {v.dtype})")
+        return get_engine(self.n_feat, self.n_cfeat, self.h, dev), P
+
+    def _invalidate_eval_pack(self):
+        self._eval_key = None
+
+    def _eval_pack_key(self, P):
+        return tuple((v.data_ptr(), v._version) for v in P.values())
+
+    def draw_shortcut(self, device, n_sets: int = 1):
+        """Fresh 1x1 shortcut (diffusion_utilities.py:54).  Returns (w [n_sets*nf], b [n_sets*nf])."""
+        nf = self.n_feat
+        if self.shortcut_source == "cpu":
+            ws, bs = [], []
+            for _ in range(n_sets):
+                conv = nn.Conv2d(self.in_channels, nf, kernel_size=1, stride=1, padding=0)
+                ws.append(conv.weight.detach().reshape(nf)); bs.append(conv.bias.detach())
+            return torch.cat(ws).to(device), torch.cat(bs).to(device)
+        from ._lib import lib
+        w = torch.empty(2 * n_sets * nf, device=device)
+        self._sc_counter += 1
+        lib().cdm_philox_uniform(w.data_ptr(), w.numel(), -1.0, 1.0, 0x5C0FFEE + id(self) % 65536,
+                                 self._sc_counter, _stream())
+        return w[: n_sets * nf], w[n_sets * nf:]
+
+    # -------------------------------------------------------------------------------------------
+    def forward(self, x, t, c=None):
+        """x [B,1,H,W]; t in [0,1] with B or 1 elements (any shape); c [B|1, n_cfeat] or None (zeros)."""
+        eng, P = self._engine_and_params()
+        dev = x.device
+        B = x.shape[0]
+        x = x.to(torch.float32).contiguous()
+        t = torch.as_tensor(t).to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+        if c is not None:
+            c = c.to(device=dev, dtype=torch.float32).reshape(-1, self.n_cfeat).contiguous()
+        sc_w, sc_b = self.draw_shortcut(dev)
+        needs_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        if self.training and needs_grad:
+            return _UNetFunction.apply((self,), x, t, c, sc_w, sc_b, *[P[n] for n in self._param_names])
+        if needs_grad and not self.training:
+            raise NotImplementedError("gradients through eval-mode BatchNorm are not on the reference path; "
+                                      "use torch.no_grad() for eval forwards")
+        s = _stream()
+        train = self.training
+        if train:
+            eng.repack(P, True, s)
+            self._invalidate_eval_pack()
+        else:
+            key = self._eval_pack_key(P)
+            eng.repack(P, False, s, key=key)
+        ws = _cached_ws(eng, B, train)
+        eps = torch.empty(B, 1, self.h, self.h, device=dev)
+        eng.forward(ws, P, x.reshape(B, self.h, self.h), t, c, sc_w, sc_b, B, s, out=eps.view(B, self.h, self.h))
+        return eps
+
+
+_WS: Dict[tuple, object] = {}
+
+
+def _cached_ws(eng, B, train):
+    key = (id(eng), B, train)
+    ws = _WS.get(key)
+    if ws is None:
+        if len(_WS) > 8:
+            _WS.clear()
+        ws = _WS[key] = eng.workspace(B, train)
+    return ws

@@ -1,0 +1,142 @@
+/*
+ * cdm_hip.h — C ABI of libcdm_hip.so, the MI355X (gfx950) kernels behind the ContextUnet DDPM
+ * hot path.  Plain pointers and sizes only (no torch types).  Every function returns 0 on success
+ * or a hipError_t code; launches go on the caller's stream (`stream` is a hipStream_t, NULL =
+ * default stream); the library never allocates, never synchronises and keeps no global state, so
+ * every call can be captured into a hipGraph.
+ *
+ * The reference has no FFI: its boundary is the Python module API.  Each entry point
+ * below names the reference operation it replaces (paths relative to the reference repo root).
+ * Layout: activations NHWC fp32, (N,H,W,C) with a pixel stride `ld*` >= C so that channel slices
+ * of concatenation buffers are addressable (replaces torch.cat, diffusion_utilities.py:96 and
+ * ContextUnet.py:59).  Weights are the reference OIHW / ConvTranspose [Cin][Cout][kh][kw] tensors
+ * repacked by cdm_pack_* into GEMM layouts.
+ */
+#ifndef CDM_HIP_H
+#define CDM_HIP_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CDM_EPI_RELU 1
+#define CDM_EPI_ACCUM 2
+
+int cdm_abi_version(void);
+int cdm_device_sync(void);
+
+/* ---- contractions (fp32 MFMA 32x32x2; csrc/gemm_f32.hip) -------------------------------------- */
+/* nn.Conv2d(Cin,Cout,3,1,1) forward (diffusion_utilities.py:27,34; ContextUnet.py:36) and, with
+ * flipped weights, its input gradient.  y (+)= conv(x) + bias; stats[tile][2][stats_ld] receives
+ * per-128-pixel column sums / sums of squares (BatchNorm2d batch statistics, diffusion_utilities.py:28). */
+int cdm_conv3x3_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk, const float* bias,
+                    float* y, int ldy, int Cout, int flags, float* stats, int stats_ld, void* stream);
+/* nn.ConvTranspose2d(Cin,Cout,2,2) forward (diffusion_utilities.py:86); H,W = input grid. */
+int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk, const float* bias,
+                     float* y, int ldy, int Cout, void* stream);
+/* its input gradient (autograd of diffusion_utilities.py:86). */
+int cdm_convT2x2_dgrad(const float* dy, int N, int H, int W, int Cout, int lddy, const float* wpkT, float* dx,
+                       int lddx, int Cin, int flags, void* stream);
+/* dense C = A.B (+bias[n % bias_mod]): up0 ConvTranspose2d(2nf,2nf,h/4,h/4) on a 1x1 map (ContextUnet.py:27)
+ * and its input gradient (split-K partial slabs when splits > 1). */
+int cdm_gemm_f32(const float* a, long long lda, int M, int K, const float* b, long long ldb, int N, float* c,
+                 long long ldc, const float* bias, int bias_mod, int flags, int splits, float* slab, void* stream);
+int cdm_gemm_splits(int K, int splits);
+/* weight gradients (autograd of the layers above), split-K partial slabs [splits][M][N]. */
+int cdm_conv3x3_wgrad(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,
+                      int splits, float* slab, void* stream);
+int cdm_convT2x2_wgrad(const float* x, int N, int H, int W, int Cin, int ldx, const float* dy, int Cout, int lddy,
+                       int splits, float* slab, void* stream);
+int cdm_gemm_tn_f32(const float* a, long long lda, int M, int K, const float* b, long long ldb, int N, int splits,
+                    float* slab, void* stream);
+/* out[m*s_m + (n/csplit)*s_hi + (n%csplit)*s_lo] (+)= scale * sum_z slab[z][m][n] */
+int cdm_slab_reduce(const float* slab, int splits, int M, int N, float* out, long long s_m, long long s_hi,
+                    long long s_lo, int csplit, int accumulate, float scale, void* stream);
+
+/* ---- normalisation / pooling / FiLM (csrc/norm.hip) ------------------------------------------- */
+/* per-(image, pixel-chunk) partial sums (slab[N][chunks][R][C]) */
+int cdm_reduce_stats(const float* y, int ldy, int N, int HW, int C, int csize, float* slab, void* stream);
+int cdm_reduce_sum(const float* g, int ldg, int N, int HW, int C, int csize, float* slab, void* stream);
+/* BatchNorm2d / GroupNorm(8) + ReLU (+MaxPool2d(2) | +FiLM) backward sums (mode 0 plain, 1 pool, 2 FiLM) */
+int cdm_norm_bwd_reduce(int mode, const float* g, int ldg, const float* y, int ldy, int N, int H, int W, int C,
+                        const float* s, const float* t, int sn, const float* mean, const float* invstd, int mn,
+                        int cpg, const float* film_a, int film_an, int csize, float* slab, void* stream);
+/* BatchNorm2d train statistics + running-stat update (diffusion_utilities.py:28,35; momentum 0.1, eps 1e-5) */
+int cdm_bn_fwd_finalize(const float* slab, int ntiles, int R, int C, double count, const float* gamma,
+                        const float* beta, float* rmean, float* rvar, long long* nbt, float momentum, float eps,
+                        float* mean, float* invstd, float* scale, float* shift, void* stream);
+/* BatchNorm2d eval (running statistics) */
+int cdm_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
+                       float* mean, float* invstd, float* scale, float* shift, void* stream);
+/* GroupNorm(8, C) statistics (ContextUnet.py:28,37) */
+int cdm_gn_fwd_finalize(const float* slab, int N, int nchunks, int R, int C, int G, double count, const float* gamma,
+                        const float* beta, float eps, float* mean, float* invstd, float* scale, float* shift,
+                        void* stream);
+int cdm_bn_bwd_finalize(const float* slab, int ntiles, int C, double count, const float* gamma, const float* invstd,
+                        float* dgamma, float* dbeta, float* A, float* B, float* Cc, float* dbias, void* stream);
+int cdm_gn_bwd_finalize(const float* slab, int N, int nchunks, int C, int G, double count_g, int HW,
+                        const float* gamma, const float* invstd, float* A, float* B, float* Cc, float* pdg, float* pdb,
+                        float* pdbias, void* stream);
+int cdm_slab_sum_nc(const float* slab, int N, int nchunks, int R, int r, int C, float* out, void* stream);
+int cdm_col_sum(const float* in, int N, int C, float* out, int accumulate, void* stream);
+/* out = [MaxPool2d(2)]([cemb*](ReLU(y*s+t))[+temb])[+ 1x1 shortcut(x)]  — flags 1 pool, 2 FiLM, 4 resid, 8 relu
+ * (BN/GN apply diffusion_utilities.py:28-29; MaxPool2d :109; random shortcut :54-55; FiLM ContextUnet.py:57-58) */
+int cdm_norm_apply_fwd(int flags, const float* y, int ldy, int N, int H, int W, int C, const float* s, const float* t,
+                       int sn, const float* film_a, int film_an, const float* film_b, int film_bn, const float* rx,
+                       const float* rw, const float* rb, int rsplit, float* out, int ldo, void* stream);
+int cdm_norm_apply_bwd(int mode, const float* g, int ldg, const float* y, int ldy, int N, int H, int W, int C,
+                       const float* s, const float* t, int sn, const float* mean, const float* invstd, int mn, int cpg,
+                       const float* film_a, int film_an, const float* A, const float* B, const float* Cc, int cn,
+                       float* dy, int lddy, void* stream);
+
+/* ---- small ops (csrc/misc.hip) ---------------------------------------------------------------- */
+/* init_conv.conv1: Conv2d(1, nf, 3, 1, 1) (ContextUnet.py:14 -> diffusion_utilities.py:27) */
+int cdm_conv3x3_cin1_fwd(const float* x, int N, int H, int W, const float* wt, const float* bias, float* y, int ldy,
+                         int C, int relu, void* stream);
+int cdm_conv3x3_cin1_wgrad(const float* dy, int lddy, const float* x, int N, int H, int W, int C, int csize,
+                           float* slab, void* stream);
+int cdm_slab_sum_all(const float* slab, int ntiles, int R, int r0, int rn, int C, float* out, long long s_r,
+                     long long s_c, int accumulate, void* stream);
+/* out.3: Conv2d(nf, 1, 3, 1, 1) (ContextUnet.py:39) */
+int cdm_conv3x3_cout1_fwd(const float* z, int ldz, int N, int H, int W, int C, const float* w, const float* bias,
+                          float* out, void* stream);
+int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int C, const float* w, float* dz, int lddz,
+                            void* stream);
+int cdm_conv3x3_cout1_wgrad(const float* deps, const float* z, int ldz, int N, int H, int W, int C, int csize,
+                            float* slab, void* stream);
+/* to_vec: AvgPool2d(h/4) + GELU (ContextUnet.py:17) */
+int cdm_avgpool_gelu_fin(const float* sums, int N, int C, int HW, float* hpre, float* hv, void* stream);
+int cdm_avgpool_gelu_bwd(const float* dhv, const float* hpre, int N, int HW, int C, float* dst, int ldd, void* stream);
+/* EmbedFC x4 (diffusion_utilities.py:118-145); `P` points to a host struct cdm_mlp4 (see csrc/misc.hip MlpDesc) */
+int cdm_embed_fwd(const void* P, void* stream);
+int cdm_embed_bwd(const void* P, void* stream);
+/* perturb_input (code/train_diffusion_condition.py:202-203) + t/T for the time embedding (:225) */
+int cdm_perturb(const float* x, const float* noise, const int* t, const float* sab, const float* omab, int N, int HW,
+                int T, float* out, float* tin, void* stream);
+/* F.mse_loss + its gradient (code/train_diffusion_condition.py:227) */
+int cdm_mse(const float* pred, const float* noise, long long n, float* dpred, float* partial, int nb, float* loss_out,
+            float* dbias_out, void* stream);
+/* sampler: per-step prologue (device step counter) and denoise_add_noise + CFG combine
+ * (code/train_diffusion_condition.py:274-279, 312-333) */
+int cdm_sample_prologue(int* ctr, int T, int* cur_i, float* t_cur, const float* sc_table, int sc_row, float* sc_cur,
+                        void* stream);
+int cdm_denoise(float* x, float* x2, long long numel, const float* eps, int cfg, float w, const int* cur_i,
+                const float* coef, const float* sa, const float* sb, const float* z_table, unsigned long long seed,
+                const int* snap_slot, float* snaps, int T, void* stream);
+/* randn_like / randint / the per-forward random 1x1 shortcut draw (diffusion_utilities.py:54), on-device Philox */
+int cdm_philox_normal(float* out, long long n, unsigned long long seed, unsigned int sub, void* stream);
+int cdm_philox_uniform(float* out, long long n, float lo, float hi, unsigned long long seed, unsigned int sub,
+                       void* stream);
+int cdm_philox_randint(int* out, int n, int lo, int hi, unsigned long long seed, unsigned int sub, void* stream);
+/* torch.optim.Adam step (code/train_diffusion_condition.py:200,229); state = {lr, step, -, -} in device memory */
+int cdm_adam(float* p, const float* g, float* m, float* v, long long n, float* state, double beta1, double beta2,
+             double eps, void* stream);
+/* weight repacking (+ eval-mode BatchNorm folding) */
+int cdm_pack_conv3x3(const float* W, const float* b, int Cin, int Cout, const float* gamma, const float* beta,
+                     const float* rm, const float* rv, float eps, float* wpk, float* bpk, float* wdg, void* stream);
+int cdm_pack_convT(const float* W, int Cin, int Cout, int KK, float* wt, float* wtT, void* stream);
+int cdm_transpose(const float* in, int R, int C, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CDM_HIP_H */

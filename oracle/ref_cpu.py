@@ -112,7 +112,7 @@ class _Ctx:
         return F.conv2d(x, w, b) + x2
 
     def embed(self, v, name, in_dim):
-        v = v.reshape(-1, in_dim)
+        v = v.reshape(-1, in_dim).to(self.sd[name + ".model.0.weight"].dtype)
         h = F.linear(v, self.sd[name + ".model.0.weight"], self.sd[name + ".model.0.bias"])
         h = F.gelu(h)
         return F.linear(h, self.sd[name + ".model.2.weight"], self.sd[name + ".model.2.bias"])
@@ -209,7 +209,7 @@ def state_dict_layout(in_channels: int, n_feat: int, n_cfeat: int, height: int):
 
 
 def clone_sd(sd):
-    return {k: v.detach().clone() for k, v in sd.items()}
+    return {k: v.detach().cpu().clone() for k, v in sd.items()}
 
 
 # ----------------------------------------------------------------------------------------------

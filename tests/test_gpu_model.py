@@ -1,0 +1,177 @@
+"""Whole-model parity of the HIP ContextUnet against the CPU oracle / reference golden vectors.
+
+Tolerances (fp32 everywhere; only summation order differs):
+  forward eps            max|d| <= 1e-4 * max|ref|
+  parameter gradients    per tensor  max|d| <= 2e-3 * max|ref| + 1e-4 * max over all grads of max|ref|
+  BN running stats       max|d| <= 1e-5 * max|ref| + 1e-6
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ref_cpu as R
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _model(nf, ncf=6, sd=None, seed=0):
+    from cdm_amd import ContextUnet
+    torch.manual_seed(seed)
+    m = ContextUnet(1, nf, ncf, 64)
+    if sd is not None:
+        m.load_state_dict({k: torch.as_tensor(v) for k, v in sd.items()})
+    return m.cuda()
+
+
+def _fx(name):
+    return np.load(os.path.join(GOLD, name))
+
+
+def _sd(fx, prefix="sd."):
+    return {k[len(prefix):]: torch.from_numpy(fx[k].copy()) for k in fx.files if k.startswith(prefix)}
+
+
+def _rel(got, ref):
+    got = got.detach().float().cpu(); ref = ref.detach().float().cpu()
+    return (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
+
+
+@pytest.mark.parametrize("nf", [8, 16])
+def test_eval_forward_matches_reference(nf):
+    fx = _fx(f"model_nf{nf}.npz")
+    m = _model(nf, sd=_sd(fx)).eval()
+    x, t, c = (torch.from_numpy(fx[k]).cuda() for k in ("x", "t", "c"))
+    with torch.no_grad():
+        torch.manual_seed(11)                 # the reference drew its shortcut from this seed
+        eps = m(x, t, c)
+        assert _rel(eps, torch.from_numpy(fx["eval_eps"])) < 1e-4
+        torch.manual_seed(12)
+        t1 = torch.tensor([0.37])[:, None, None, None].cuda()
+        eps = m(x, t1, None)
+        assert _rel(eps, torch.from_numpy(fx["eval_uncond_eps"])) < 1e-4
+
+
+def test_train_step_grads_match_reference():
+    fx = _fx("model_nf8.npz")
+    nf, T = 8, int(fx["train_T"])
+    m = _model(nf, sd=_sd(fx)).train()
+    c = torch.from_numpy(fx["c"]).cuda()
+    xp = torch.from_numpy(fx["train0_xpert"]).cuda()
+    noise = torch.from_numpy(fx["train0_noise"]).cuda()
+    tt = torch.from_numpy(fx["train0_t"]).cuda()
+    torch.manual_seed(100)
+    torch.randn(fx["x"].shape); torch.randint(1, T + 1, (fx["x"].shape[0],))  # replay the RNG order of the loop
+    pred = m(xp, tt / T, c)
+    loss = F.mse_loss(pred, noise)
+    loss.backward()
+    assert _rel(pred, torch.from_numpy(fx["train0_eps"])) < 1e-4
+    assert abs(loss.item() - float(fx["train0_loss"])) <= 1e-5 * float(fx["train0_loss"])
+    gmax = max(np.abs(fx["train0_grad." + k]).max() for k, _ in m.named_parameters())
+    worst = []
+    for k, p in m.named_parameters():
+        ref = torch.from_numpy(fx["train0_grad." + k])
+        err = (p.grad.cpu() - ref).abs().max().item()
+        bound = 2e-3 * ref.abs().max().item() + 1e-4 * gmax
+        worst.append((err / bound, k, err, ref.abs().max().item()))
+        assert err <= bound, f"{k}: err {err:.3e} bound {bound:.3e}"
+    print("worst grad ratios", sorted(worst)[-5:])
+
+
+def test_running_stats_update():
+    fx = _fx("model_nf8.npz")
+    sd = _sd(fx)
+    m = _model(8, sd=sd).train()
+    x, t, c = (torch.from_numpy(fx[k]).cuda() for k in ("x", "t", "c"))
+    with torch.no_grad():
+        torch.manual_seed(5)
+        m(x, t, c)
+    osd = R.clone_sd(sd)
+    torch.manual_seed(5)
+    R.unet_forward(osd, x.cpu(), t.cpu(), c.cpu(), n_feat=8, n_cfeat=6, height=64, train=True,
+                   shortcut=lambda: R.draw_shortcut(1, 8))
+    for k, v in m.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            ref = osd[k].float()
+            err = (v.cpu().float() - ref).abs().max().item()
+            assert err <= 1e-5 * ref.abs().max().item() + 1e-6, k
+
+
+@pytest.mark.parametrize("nf,B", [(64, 3), (128, 2)])
+def test_forward_random_weights_vs_oracle(nf, B):
+    m = _model(nf, seed=3)
+    g = torch.Generator().manual_seed(9)
+    x = torch.rand(B, 1, 64, 64, generator=g); t = torch.rand(B, generator=g); c = torch.rand(B, 6, generator=g)
+    sd = R.clone_sd(m.state_dict())
+    for train in (False, True):
+        m.train(train)
+        with torch.no_grad():
+            torch.manual_seed(21)
+            eps = m(x.cuda(), t.cuda(), c.cuda())
+        torch.manual_seed(21)
+        ref = R.unet_forward(R.clone_sd(sd), x, t, c, n_feat=nf, n_cfeat=6, height=64, train=train,
+                             shortcut=lambda: R.draw_shortcut(1, nf))
+        assert _rel(eps, ref) < 2e-4, (train, _rel(eps, ref))
+
+
+def _oracle_grads(sd, x, c, noise, tt, T, ab, nf, dtype, seed):
+    s = {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+    tr = R.OracleTrainer(s, n_feat=nf, n_cfeat=6, height=64)
+    torch.manual_seed(seed)
+    w, b = R.draw_shortcut(1, nf)
+    _, pred, grads = tr.step(x.to(dtype), c.to(dtype), noise.to(dtype), tt, T, ab.to(dtype),
+                             (w.to(dtype), b.to(dtype)))
+    return pred, grads
+
+
+def test_train_grads_random_weights_nf64():
+    """HIP grads vs an fp64 oracle, at the accuracy the reference's own fp32 CPU path has.
+
+    Rationale: with ReLU + MaxPool, last-bit differences flip a handful of kink decisions (|z| ~ 1e-6)
+    and each flip propagates to every layer upstream of it.  For this very input the reference CPU
+    path in fp32 vs fp64 shows relative-L2 errors up to 3.8e-3 (a flip in down2), the HIP path up to
+    4.1e-3 (a flip in up2).  Criterion, relative L2 vs fp64: every tensor <= 1e-2, and the median
+    over tensors <= 5e-3.  Conv biases feeding a BatchNorm have an analytic gradient of 0 (rounding
+    noise only): |g| <= 1e-4 * max grad.  The strict check lives in test_train_step_grads_match_reference.
+    """
+    nf, B, T = 64, 2, 1500
+    m = _model(nf, seed=4).train()
+    sd = R.clone_sd(m.state_dict())
+    g = torch.Generator().manual_seed(10)
+    x = torch.rand(B, 1, 64, 64, generator=g); noise = torch.randn(B, 1, 64, 64, generator=g)
+    c = torch.rand(B, 6, generator=g); tt = torch.randint(1, T + 1, (B,), generator=g)
+    _, _, ab = R.make_schedule(T)
+    xp = R.perturb_input(x, tt, noise, ab)
+    torch.manual_seed(33)
+    pred = m(xp.cuda(), (tt / T).cuda(), c.cuda())
+    F.mse_loss(pred, noise.cuda()).backward()
+    p32, g32 = _oracle_grads(sd, x, c, noise, tt, T, ab, nf, torch.float32, 33)
+    p64, g64 = _oracle_grads(sd, x, c, noise, tt, T, ab, nf, torch.float64, 33)
+    assert _rel(pred.double(), p64) < 2e-4
+    gmax = max(v.abs().max().item() for v in g64.values())
+    bad, errs = [], []
+    for k, p in m.named_parameters():
+        ref = g64[k]
+        got = p.grad.cpu().double()
+        if ".conv1.0.bias" in k or ".conv2.0.bias" in k:
+            ok = got.abs().max().item() <= 1e-4 * gmax
+            print(f"{k:40s} |g| {got.abs().max().item():.2e} (analytic 0)")
+        else:
+            e_hip = ((got - ref).norm() / ref.norm()).item()
+            e_cpu = ((g32[k].double() - ref).norm() / ref.norm()).item()
+            ok = e_hip <= 1e-2
+            errs.append(e_hip)
+            print(f"{k:40s} l2rel hip {e_hip:.2e} cpu32 {e_cpu:.2e}")
+        if not ok:
+            bad.append(k)
+    assert not bad, bad
+    assert float(np.median(errs)) <= 5e-3
