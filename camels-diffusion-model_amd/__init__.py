@@ -5,6 +5,9 @@ Drop-in for the reference's ContextUnet module API (ContextUnet.py), its diffusi
 repo-root ``cdm_amd.py`` shim maps the hyphenated directory to that name).
 """
 from ._lib import lib  # noqa: F401
+from .diffusion import DDPM, GraphSampler, Schedule, denoise_add_noise, perturb_input, sample_ddpm  # noqa: F401
 from .model import ContextUnet, EmbedFC, ResidualConvBlock, UnetDown, UnetUp  # noqa: F401
+from .trainer import Trainer  # noqa: F401
 
-__all__ = ["ContextUnet", "EmbedFC", "ResidualConvBlock", "UnetDown", "UnetUp", "lib"]
+__all__ = ["ContextUnet", "EmbedFC", "ResidualConvBlock", "UnetDown", "UnetUp", "lib", "DDPM", "GraphSampler",
+           "Schedule", "denoise_add_noise", "perturb_input", "sample_ddpm", "Trainer"]

@@ -34,8 +34,9 @@ struct LdDenseA {  // A[m][k] = a[m*lda + k]
     }
 };
 
+template <int CT>  // CT > 0: channel count known at compile time (the 128-feature hot conv)
 struct LdIm2colA {  // 3x3, stride 1, pad 1; m = (n,h,w), k = (ky*3+kx)*C + ci
-    const float* x; int H, W, C, ldx, M, K;
+    const float* x; int H, W, Crt, ldx, M, K;
     struct Row { int n, h, w; bool ok; };
     __device__ __forceinline__ Row row(int m) const {
         Row r; r.ok = m < M; const int hw = H * W; r.n = m / hw; const int rem = m - r.n * hw;
@@ -43,6 +44,7 @@ struct LdIm2colA {  // 3x3, stride 1, pad 1; m = (n,h,w), k = (ky*3+kx)*C + ci
     }
     __device__ __forceinline__ float4 load(const Row& r, int k) const {
         if (!r.ok || k >= K) return f4zero();
+        const int C = CT > 0 ? CT : Crt;
         const int tap = k / C, ci = k - tap * C;
         const int ky = tap / 3, kx = tap - ky * 3;
         const int hh = r.h + ky - 1, ww = r.w + kx - 1;
@@ -327,10 +329,14 @@ CDM_API int cdm_conv3x3_fwd(const float* x, int N, int H, int W, int Cin, int ld
                             void* stream) {
     if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
     const int M = N * H * W, K = 9 * Cin;
-    LdIm2colA la{x, H, W, Cin, ldx, M, K};
     LdDenseB lb{wpk, Cout, K, Cout};
     EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout};
-    return launch_gemm<LdIm2colA, LdDenseB, EpiStore, false>(la, lb, ep, M, Cout, K, 1, S(stream));
+    if (Cin == 128 && Cout == 128) {   // the 128-feature hot conv: its own (compile-time C) instantiation
+        LdIm2colA<128> la{x, H, W, Cin, ldx, M, K};
+        return launch_gemm<LdIm2colA<128>, LdDenseB, EpiStore, false>(la, lb, ep, M, Cout, K, 1, S(stream));
+    }
+    LdIm2colA<0> la{x, H, W, Cin, ldx, M, K};
+    return launch_gemm<LdIm2colA<0>, LdDenseB, EpiStore, false>(la, lb, ep, M, Cout, K, 1, S(stream));
 }
 
 CDM_API int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,

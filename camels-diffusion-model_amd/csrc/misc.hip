@@ -53,7 +53,9 @@ static __device__ __forceinline__ float philox_normal(unsigned long long seed, u
     return j == 0 ? z0 : (j == 1 ? z1 : (j == 2 ? z2 : z3));
 }
 
-__global__ void philox_uniform_kernel(float* out, long long n, float lo, float hi, unsigned long long seed, uint32_t sub) {
+__global__ void philox_uniform_kernel(float* out, long long n, float lo, float hi, unsigned long long seed, uint32_t sub,
+                                      const int* sub_dev) {
+    if (sub_dev) sub += (uint32_t)*sub_dev;
     for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q * 4 < n; q += (long long)gridDim.x * blockDim.x) {
         const U4 v = philox((uint32_t)q, (uint32_t)((unsigned long long)q >> 32), sub, 0x0417u, (uint32_t)seed,
                             (uint32_t)(seed >> 32));
@@ -62,7 +64,8 @@ __global__ void philox_uniform_kernel(float* out, long long n, float lo, float h
     }
 }
 
-__global__ void philox_normal_kernel(float* out, long long n, unsigned long long seed, uint32_t sub) {
+__global__ void philox_normal_kernel(float* out, long long n, unsigned long long seed, uint32_t sub, const int* sub_dev) {
+    if (sub_dev) sub += (uint32_t)*sub_dev;
     for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q * 4 < n; q += (long long)gridDim.x * blockDim.x) {
         const U4 v = philox((uint32_t)q, (uint32_t)((unsigned long long)q >> 32), sub, 0x5EEDu, (uint32_t)seed,
                             (uint32_t)(seed >> 32));
@@ -73,7 +76,9 @@ __global__ void philox_normal_kernel(float* out, long long n, unsigned long long
 }
 
 // t[n] in [lo, hi] uniformly (torch.randint(1, T+1) equivalent distribution)
-__global__ void philox_randint_kernel(int* out, int n, int lo, int hi, unsigned long long seed, uint32_t sub) {
+__global__ void philox_randint_kernel(int* out, int n, int lo, int hi, unsigned long long seed, uint32_t sub,
+                                      const int* sub_dev) {
+    if (sub_dev) sub += (uint32_t)*sub_dev;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const U4 v = philox((uint32_t)i, 0x71u, sub, 0xA11Cu, (uint32_t)seed, (uint32_t)(seed >> 32));
@@ -362,11 +367,12 @@ __global__ __launch_bounds__(256) void embed_bwd_param_kernel(Mlp4 P) {
 // x_pert = sqrt(ab[t]) x + (1 - ab[t]) noise ; temb_in = float(t)/float(T)
 __global__ void perturb_kernel(const float* x, const float* noise, const int* t, const float* sab, const float* omab,
                                int N, int HW, float T, float* out, float* tin) {
+#pragma clang fp contract(off)  // keep the reference's separate fp32 roundings (bit-exact)
     const long long total = (long long)N * HW;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
         const int n = (int)(i / HW);
         const int ti = t[n];
-        out[i] = sab[ti] * x[i] + omab[ti] * noise[i];
+        out[i] = sab[ti] * x[i] + omab[ti] * noise[i];  // two roundings + one, as the reference (contract off)
         if (tin && i - (long long)n * HW == 0) tin[n] = (float)ti / T;
     }
 }
@@ -413,9 +419,11 @@ __global__ void sample_prologue_kernel(int* ctr, int T, int* cur_i, float* t_cur
 // x <- (x - eps*coef[i]) / sa[i] + sb[i]*z ;  eps = eu + w (ec - eu) when cfg (model batch = 2n)
 // z = 0 at i == 1; z from z_table[(T-i)][e] when given, else Philox(seed, stream i).
 // Writes x into both halves of the model-input buffer (x2 may alias x), and a snapshot when slot[i] >= 0.
-__global__ void denoise_kernel(float* x, float* x2, long long numel, const float* eps, int cfg, float w,
-                               const int* cur_i, const float* coef, const float* sa, const float* sb,
-                               const float* z_table, unsigned long long seed, const int* snap_slot, float* snaps, int T) {
+__global__ void denoise_kernel(const float* xin, float* x, float* x2, long long numel, const float* eps, int cfg,
+                               float w, const int* cur_i, const float* coef, const float* sa, const float* sb,
+                               const float* z_table, long long zstride, unsigned long long seed, const int* snap_slot,
+                               float* snaps, int T) {
+#pragma clang fp contract(off)  // keep the reference's separate fp32 roundings (bit-exact)
     const int i = *cur_i;
     const float cf = coef[i], a = sa[i], b = sb[i];
     const int slot = snap_slot ? snap_slot[i] : -1;
@@ -423,8 +431,8 @@ __global__ void denoise_kernel(float* x, float* x2, long long numel, const float
         float ep = eps[e];
         if (cfg) { const float eu = eps[numel + e]; ep = eu + w * (ep - eu); }
         float z = 0.f;
-        if (i > 1) z = z_table ? z_table[(long long)(T - i) * numel + e] : philox_normal(seed, (uint32_t)i, e);
-        const float mean = (x[e] - ep * cf) / a;
+        if (i > 1) z = z_table ? z_table[(long long)(T - i) * zstride + e] : philox_normal(seed, (uint32_t)i, e);
+        const float mean = (xin[e] - ep * cf) / a;   // same op order / roundings as the reference
         const float v = mean + b * z;
         x[e] = v;
         if (x2) { x2[e] = v; x2[numel + e] = v; }
@@ -444,14 +452,15 @@ __global__ void adam_prep_kernel(float* state, double beta1, double beta2) {
     state[3] = (float)sqrt(bc2);
 }
 __global__ void adam_kernel(float* p, const float* g, float* m, float* v, long long n, const float* state, float beta1c,
-                            float beta2, float beta2c, float eps) {
+                            float beta2, float beta2c, float eps, float gscale) {
+#pragma clang fp contract(off)  // keep the reference's separate fp32 roundings (bit-exact)
     const float nss = state[2], bc2s = state[3];
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-        const float gi = g[i];
+        const float gi = g[i] * gscale;             // 1/world for the summed data-parallel gradient
         float mi = m[i];
         mi = mi + beta1c * (gi - mi);                    // exp_avg.lerp_(grad, 1 - beta1)
         float vi = v[i] * beta2;                          // exp_avg_sq.mul_(beta2)
-        vi = vi + beta2c * gi * gi;                       //           .addcmul_(grad, grad, 1 - beta2)
+        vi = vi + beta2c * gi * gi;                       //   .addcmul_(grad, grad, 1 - beta2)
         const float denom = sqrtf(vi) / bc2s + eps;       // (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
         p[i] = p[i] + nss * (mi / denom);                 // param.addcdiv_(exp_avg, denom, -step_size)
         m[i] = mi; v[i] = vi;
@@ -515,17 +524,21 @@ using namespace cdm;
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ------------------------------------------ C ABI ------------------------------------------------
-CDM_API int cdm_philox_normal(float* out, long long n, unsigned long long seed, unsigned int sub, void* stream) {
-    hipLaunchKernelGGL(philox_normal_kernel, dim3(nblocks((n + 3) / 4)), dim3(256), 0, S(stream), out, n, seed, sub);
+CDM_API int cdm_philox_normal(float* out, long long n, unsigned long long seed, unsigned int sub, const int* sub_dev,
+                              void* stream) {
+    hipLaunchKernelGGL(philox_normal_kernel, dim3(nblocks((n + 3) / 4)), dim3(256), 0, S(stream), out, n, seed, sub, sub_dev);
     return cdm_status();
 }
 CDM_API int cdm_philox_uniform(float* out, long long n, float lo, float hi, unsigned long long seed, unsigned int sub,
-                               void* stream) {
-    hipLaunchKernelGGL(philox_uniform_kernel, dim3(nblocks((n + 3) / 4)), dim3(256), 0, S(stream), out, n, lo, hi, seed, sub);
+                               const int* sub_dev, void* stream) {
+    hipLaunchKernelGGL(philox_uniform_kernel, dim3(nblocks((n + 3) / 4)), dim3(256), 0, S(stream), out, n, lo, hi, seed, sub,
+                       sub_dev);
     return cdm_status();
 }
-CDM_API int cdm_philox_randint(int* out, int n, int lo, int hi, unsigned long long seed, unsigned int sub, void* stream) {
-    hipLaunchKernelGGL(philox_randint_kernel, dim3((n + 255) / 256), dim3(256), 0, S(stream), out, n, lo, hi, seed, sub);
+CDM_API int cdm_philox_randint(int* out, int n, int lo, int hi, unsigned long long seed, unsigned int sub,
+                               const int* sub_dev, void* stream) {
+    hipLaunchKernelGGL(philox_randint_kernel, dim3((n + 255) / 256), dim3(256), 0, S(stream), out, n, lo, hi, seed, sub,
+                       sub_dev);
     return cdm_status();
 }
 CDM_API int cdm_conv3x3_cin1_fwd(const float* x, int N, int H, int W, const float* w9, const float* bias, float* y,
@@ -618,19 +631,20 @@ CDM_API int cdm_sample_prologue(int* ctr, int T, int* cur_i, float* t_cur, const
                        sc_cur);
     return cdm_status();
 }
-CDM_API int cdm_denoise(float* x, float* x2, long long numel, const float* eps, int cfg, float w, const int* cur_i,
-                        const float* coef, const float* sa, const float* sb, const float* z_table,
-                        unsigned long long seed, const int* snap_slot, float* snaps, int T, void* stream) {
-    hipLaunchKernelGGL(denoise_kernel, dim3(nblocks(numel)), dim3(256), 0, S(stream), x, x2, numel, eps, cfg, w, cur_i, coef,
-                       sa, sb, z_table, seed, snap_slot, snaps, T);
+CDM_API int cdm_denoise(const float* xin, float* x, float* x2, long long numel, const float* eps, int cfg, float w,
+                        const int* cur_i, const float* coef, const float* sa, const float* sb, const float* z_table,
+                        long long zstride, unsigned long long seed, const int* snap_slot, float* snaps, int T,
+                        void* stream) {
+    hipLaunchKernelGGL(denoise_kernel, dim3(nblocks(numel)), dim3(256), 0, S(stream), xin, x, x2, numel, eps, cfg, w, cur_i,
+                       coef, sa, sb, z_table, zstride, seed, snap_slot, snaps, T);
     return cdm_status();
 }
 CDM_API int cdm_adam(float* p, const float* g, float* m, float* v, long long n, float* state, double beta1, double beta2,
-                     double eps, void* stream) {
+                     double eps, float grad_scale, void* stream) {
     hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, S(stream), state, beta1, beta2);
     int e = cdm_status(); if (e) return e;
     hipLaunchKernelGGL(adam_kernel, dim3(nblocks(n, 256, 16384)), dim3(256), 0, S(stream), p, g, m, v, n, state,
-                       (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps);
+                       (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, grad_scale);
     return cdm_status();
 }
 CDM_API int cdm_pack_conv3x3(const float* W, const float* b, int Cin, int Cout, const float* gamma, const float* beta,
@@ -647,6 +661,11 @@ CDM_API int cdm_pack_convT(const float* W, int Cin, int Cout, int KK, float* wt,
 }
 CDM_API int cdm_transpose(const float* in, int R, int C, float* out, void* stream) {
     hipLaunchKernelGGL(transpose_kernel, dim3(nblocks((long long)R * C)), dim3(256), 0, S(stream), in, R, C, out);
+    return cdm_status();
+}
+__global__ void counter_add_kernel(int* c, int d) { if (threadIdx.x == 0) *c += d; }
+CDM_API int cdm_counter_add(int* ctr, int delta, void* stream) {
+    hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, S(stream), ctr, delta);
     return cdm_status();
 }
 CDM_API int cdm_device_sync() { return (int)hipDeviceSynchronize(); }

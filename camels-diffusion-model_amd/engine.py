@@ -311,8 +311,13 @@ class UNetEngine:
     # backward (train mode workspaces only)
     # ------------------------------------------------------------------------------------------
     def backward(self, ws: "Workspace", P, deps: torch.Tensor, G: Dict[str, torch.Tensor], stream: int,
-                 dbias_out3: Optional[torch.Tensor] = None):
-        """deps [B,H,W] = dL/d eps.  Writes (assigns) every parameter gradient into G[name]."""
+                 out3_bias_done: bool = False, on_stage=None):
+        """deps [B,H,W] = dL/d eps.  Writes (assigns) every parameter gradient into G[name].
+
+        ``on_stage(name)`` is called (on the host, in stream order) as soon as the gradients of a stage
+        are final: "out", "up2", "up1", "up0emb", "down2", "down1", "init" — used to start the
+        data-parallel all-reduce of that stage while the rest of the backward runs."""
+        hook = on_stage or (lambda name: None)
         assert ws.train, "backward needs a train-mode workspace"
         lb = lib(); s = stream
         nf, H, B = self.nf, self.H, ws.B
@@ -322,10 +327,8 @@ class UNetEngine:
         nch = _cdiv(H * H, CHUNK)
         lb.cdm_conv3x3_cout1_wgrad(_p(deps), _p(ws.zO), nf, B, H, H, nf, CHUNK, _p(ws.slab), s)
         lb.cdm_slab_sum_all(_p(ws.slab), B * nch, 9, 0, 9, nf, _p(G["out.3.weight"]), 1, 9, 0, s)
-        if dbias_out3 is None:
+        if not out3_bias_done:
             _sum_into(deps, G["out.3.bias"], ws.slab, s)
-        else:
-            G["out.3.bias"].copy_(dbias_out3.view_as(G["out.3.bias"]))
         gO = ws.G0
         lb.cdm_conv3x3_cout1_dgrad(_p(deps), B, H, H, nf, _p(P["out.3.weight"]), _p(gO), nf, s)
         # ---------------- out.1 GroupNorm + ReLU ----------------
@@ -336,13 +339,16 @@ class UNetEngine:
         self._wgrad3x3(ws, Act(dyO, nf), ws.catO, B, H, 2 * nf, nf, G["out.0.weight"], s)
         lb.cdm_conv3x3_fwd(_p(dyO), B, H, H, nf, nf, _p(self.pk["out.0.wdg"]), None, ws.dcatO.p, ws.dcatO.ld,
                            2 * nf, 0, None, 0, s)
+        hook("out")
         # ---------------- up2 blocks ----------------
         self._chain_bwd(ws, P, self.layers[14:18], G, s)
         # convT2 (2nf@H1 -> nf@H): grad wrt its output sits in ws.gT2
         self._convT_bwd(ws, P, "up2.model.0", Act(ws.gT2, nf), ws.catU2, B, H1, 2 * nf, nf, ws.dcatU2, G, s)
+        hook("up2")
         # ---------------- up1 blocks (last one carries FiLM2) ----------------
         self._chain_bwd(ws, P, self.layers[10:14], G, s)
         self._convT_bwd(ws, P, "up1.model.0", Act(ws.gT1, nf), ws.catU1, B, H2, 4 * nf, nf, ws.dcatU1, G, s)
+        hook("up1")
         # ---------------- up0: GroupNorm + ReLU + FiLM1 ----------------
         c0 = 2 * nf
         rows_c, rows_t = ws.c_rows, ws.t_rows
@@ -372,10 +378,14 @@ class UNetEngine:
             md.dw1 = _p(G[m + ".model.0.weight"]); md.db1 = _p(G[m + ".model.0.bias"])
             md.dw2 = _p(G[m + ".model.2.weight"]); md.db2 = _p(G[m + ".model.2.bias"])
         lb.cdm_embed_bwd(ctypes_addr(d), s)
+        hook("up0emb")
         # ---------------- down2, down1, init ----------------
         self._chain_bwd(ws, P, self.layers[6:10], G, s)
+        hook("down2")
         self._chain_bwd(ws, P, self.layers[2:6], G, s)
+        hook("down1")
         self._chain_bwd(ws, P, self.layers[0:2], G, s)
+        hook("init")
 
     def _chain_bwd(self, ws, P, layers, G, s):
         for l in reversed(layers):

@@ -186,7 +186,7 @@ class ContextUnet(nn.Module):
         w = torch.empty(2 * n_sets * nf, device=device)
         self._sc_counter += 1
         lib().cdm_philox_uniform(w.data_ptr(), w.numel(), -1.0, 1.0, 0x5C0FFEE + id(self) % 65536,
-                                 self._sc_counter, _stream())
+                                 self._sc_counter, None, _stream())
         return w[: n_sets * nf], w[n_sets * nf:]
 
     # -------------------------------------------------------------------------------------------

@@ -1,0 +1,222 @@
+"""The DDPM training step (a8) on the HIP engine, single- or multi-GPU.
+
+One step == code/train_diffusion_condition.py:216-230 (and code/train_diffusion.py:141-151):
+    noise ~ N(0,1), t ~ U{1..T}, x_pert = perturb_input(x, t, noise), eps = ContextUnet(x_pert, t/T, c)
+    (train-mode BatchNorm), loss = mse(eps, noise), backward, Adam(lr) step.
+
+MI355X design:
+  * parameters, gradients and Adam moments live in three flat fp32 buffers; the module's nn.Parameters
+    are re-pointed to views of the flat parameter buffer (state_dict stays reference-compatible);
+  * noise / timesteps / the per-forward random 1x1 shortcut come from on-device Philox keyed by a
+    device step counter, so the whole step (repack -> forward -> mse -> backward -> Adam) is captured
+    once in a hipGraph and replayed (single GPU);
+  * data parallel: one process per GPU; each rank trains on its own shard of the global batch; the
+    flat gradient buffer is laid out in backward-completion order and cut into stage buckets that are
+    all-reduced (RCCL over xGMI) asynchronously as soon as the engine reports a stage complete, so the
+    67 MB up0 gradient and everything after it overlaps the encoder's backward; BatchNorm running stats
+    are broadcast from rank 0 each step (DDP broadcast_buffers semantics), batch statistics stay local
+    to the rank (reference semantics at the local batch; no SyncBN in the reference).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ._lib import lib
+from .diffusion import Schedule
+
+STAGES: Tuple[Tuple[str, Tuple[str, ...]], ...] = (
+    ("out", ("out.",)), ("up2", ("up2.",)), ("up1", ("up1.",)),
+    ("up0emb", ("up0.", "timeembed", "contextembed")),
+    ("down2", ("down2.",)), ("down1", ("down1.",)), ("init", ("init_conv.",)),
+)
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def backward_order(names: List[str]):
+    """Parameter names in gradient-completion order, grouped by stage: [(stage, [names])]."""
+    out, seen = [], set()
+    for st, prefixes in STAGES:
+        grp = [n for n in names if n.startswith(prefixes)]
+        seen.update(grp)
+        out.append((st, grp))
+    missing = [n for n in names if n not in seen]
+    if missing:
+        raise AssertionError(f"parameters without a stage: {missing}")
+    return out
+
+
+class GradBucketer:
+    """Stage-bucketed asynchronous gradient all-reduce over a flat gradient buffer.
+
+    Device-agnostic (works with gloo on CPU tensors for tests, RCCL on MI355X)."""
+
+    def __init__(self, gflat: torch.Tensor, ranges: Dict[str, Tuple[int, int]], group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.gflat, self.ranges, self.group = gflat, ranges, group
+        self.world = dist.get_world_size(group)
+        self.pending = []
+
+    def stage_ready(self, stage: str):
+        lo, hi = self.ranges[stage]
+        if hi > lo:
+            self.pending.append(self.dist.all_reduce(self.gflat[lo:hi], op=self.dist.ReduceOp.SUM,
+                                                     group=self.group, async_op=True))
+
+    def wait(self):
+        for w in self.pending:
+            w.wait()
+        self.pending = []
+
+
+class Trainer:
+    def __init__(self, model, lrate: float, timesteps: int, batch_size: int, seed: int = 0,
+                 use_graph: bool = True, group=None, broadcast_buffers: bool = True):
+        self.model = model
+        eng, P = model._engine_and_params()
+        self.eng = eng
+        dev = P["out.3.weight"].device
+        self.dev = dev
+        self.B, self.T = int(batch_size), int(timesteps)
+        self.H, self.nf, self.ncf = model.h, model.n_feat, model.n_cfeat
+        self.group = group
+        import torch.distributed as dist
+        self.ddp = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.world = dist.get_world_size(group) if self.ddp else 1
+        self.seed = int(seed)
+        # ---- flat parameter / gradient / moment buffers in backward-completion order ----
+        names = model._param_names
+        order = backward_order(names)
+        params = dict(model.named_parameters())
+        total = sum(params[n].numel() for _, g in order for n in g)
+        self.flat = torch.empty(total, device=dev)
+        self.gflat = torch.zeros(total, device=dev)
+        self.m = torch.zeros(total, device=dev)
+        self.v = torch.zeros(total, device=dev)
+        self.views: Dict[str, torch.Tensor] = {}
+        self.grads: Dict[str, torch.Tensor] = {}
+        self.ranges: Dict[str, Tuple[int, int]] = {}
+        off = 0
+        for st, grp in order:
+            lo = off
+            for n in grp:
+                p = params[n]
+                k = p.numel()
+                view = self.flat[off:off + k].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+                self.views[n] = view
+                self.grads[n] = self.gflat[off:off + k].view_as(p)
+                off += k
+            self.ranges[st] = (lo, off)
+        self.total = total
+        # ---- BatchNorm running stats in one flat buffer (one broadcast per step under DDP) ----
+        bufs = [(n, b) for n, b in model.named_buffers() if n.endswith(("running_mean", "running_var"))]
+        self.bnflat = torch.empty(sum(b.numel() for _, b in bufs), device=dev)
+        off = 0
+        for n, b in bufs:
+            mod = model.get_submodule(n.rsplit(".", 1)[0])
+            view = self.bnflat[off:off + b.numel()]
+            view.copy_(b)
+            mod._buffers[n.rsplit(".", 1)[1]] = view
+            off += b.numel()
+        self.broadcast_buffers = broadcast_buffers
+        if self.ddp:
+            dist.broadcast(self.flat, 0, group=group)
+            dist.broadcast(self.bnflat, 0, group=group)
+            self.bucketer = GradBucketer(self.gflat, self.ranges, group)
+        # ---- optimizer state on device: [lr, step, -step_size, sqrt(bc2)] ----
+        self.opt_state = torch.tensor([float(lrate), 0.0, 0.0, 1.0], device=dev)
+        # ---- step buffers ----
+        B, HW = self.B, self.H * self.H
+        self.sched = Schedule(self.T, dev)
+        self.x0 = torch.zeros(B, self.H, self.H, device=dev)
+        self.c = torch.zeros(B, self.ncf, device=dev)
+        self.noise = torch.empty(B * HW, device=dev)
+        self.t_int = torch.empty(B, dtype=torch.int32, device=dev)
+        self.t_in = torch.empty(B, device=dev)
+        self.xpert = torch.empty(B, self.H, self.H, device=dev)
+        self.sc = torch.empty(2 * self.nf, device=dev)
+        self.deps = torch.empty(B, self.H, self.H, device=dev)
+        self.nb = 256
+        self.partial = torch.empty(2 * self.nb, device=dev)
+        self.loss = torch.zeros(1, device=dev)
+        self.ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ws = eng.workspace(B, True)
+        self.use_graph = bool(use_graph) and not self.ddp
+        self.graph = None
+        self.steps = 0
+
+    # -------------------------------------------------------------------------------------------
+    def P(self):
+        _, P = self.model._engine_and_params()
+        return P
+
+    def set_lr(self, lr: float):
+        self.opt_state[0:1].fill_(float(lr))
+
+    def _body(self, s: int):
+        lb = lib()
+        B, HW, nf = self.B, self.H * self.H, self.nf
+        P = self._P
+        seed = self.seed * 1000003 + (self._rank() << 20)
+        lb.cdm_philox_normal(_p(self.noise), B * HW, seed, 0, _p(self.ctr), s)
+        lb.cdm_philox_randint(_p(self.t_int), B, 1, self.T, seed, 1 << 24, _p(self.ctr), s)
+        lb.cdm_philox_uniform(_p(self.sc), 2 * nf, -1.0, 1.0, seed, 2 << 24, _p(self.ctr), s)
+        lb.cdm_perturb(_p(self.x0), _p(self.noise), _p(self.t_int), _p(self.sched.sab), _p(self.sched.omab), B, HW,
+                       self.T, _p(self.xpert), _p(self.t_in), s)
+        self.eng.repack(P, True, s)
+        eps = self.eng.forward(self.ws, P, self.xpert, self.t_in, self.c, self.sc[:nf], self.sc[nf:], B, s)
+        lb.cdm_mse(_p(eps), _p(self.noise), B * HW, _p(self.deps), _p(self.partial), self.nb, _p(self.loss),
+                   _p(self.grads["out.3.bias"]), s)
+        hook = self.bucketer.stage_ready if self.ddp else None
+        self.eng.backward(self.ws, P, self.deps, self.grads, s, out3_bias_done=True, on_stage=hook)
+        if self.ddp:
+            self.bucketer.wait()
+        lb.cdm_adam(_p(self.flat), _p(self.gflat), _p(self.m), _p(self.v), self.total, _p(self.opt_state), 0.9, 0.999,
+                    1e-8, 1.0 / self.world, s)
+        lb.cdm_counter_add(_p(self.ctr), 1, s)
+
+    def _rank(self):
+        if not self.ddp:
+            return 0
+        import torch.distributed as dist
+        return dist.get_rank(self.group)
+
+    def _capture(self):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self._body(torch.cuda.current_stream().cuda_stream)
+        self.graph = g
+
+    def step(self, x0: Optional[torch.Tensor] = None, c: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One training step on batch (x0 [B,1,H,H] in [0,1], c [B, n_cfeat] or None = unconditional)."""
+        if x0 is not None:
+            self.x0.copy_(x0.reshape(self.B, self.H, self.H))
+        if c is not None:
+            self.c.copy_(c.reshape(self.B, self.ncf))
+        self._P = self.P()
+        if self.ddp and self.broadcast_buffers:
+            import torch.distributed as dist
+            dist.broadcast(self.bnflat, 0, group=self.group)
+        if self.use_graph:
+            if self.graph is None:
+                self._body(_s())          # eager warm-up step (loads every kernel) then capture
+                self._capture()
+            else:
+                self.graph.replay()
+        else:
+            self._body(_s())
+        self.steps += 1
+        return self.loss

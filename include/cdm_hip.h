@@ -119,17 +119,22 @@ int cdm_mse(const float* pred, const float* noise, long long n, float* dpred, fl
  * (code/train_diffusion_condition.py:274-279, 312-333) */
 int cdm_sample_prologue(int* ctr, int T, int* cur_i, float* t_cur, const float* sc_table, int sc_row, float* sc_cur,
                         void* stream);
-int cdm_denoise(float* x, float* x2, long long numel, const float* eps, int cfg, float w, const int* cur_i,
-                const float* coef, const float* sa, const float* sb, const float* z_table, unsigned long long seed,
-                const int* snap_slot, float* snaps, int T, void* stream);
-/* randn_like / randint / the per-forward random 1x1 shortcut draw (diffusion_utilities.py:54), on-device Philox */
-int cdm_philox_normal(float* out, long long n, unsigned long long seed, unsigned int sub, void* stream);
+int cdm_denoise(const float* xin, float* x, float* x2, long long numel, const float* eps, int cfg, float w,
+                const int* cur_i, const float* coef, const float* sa, const float* sb, const float* z_table,
+                long long zstride, unsigned long long seed, const int* snap_slot, float* snaps, int T, void* stream);
+/* randn_like / randint / the per-forward random 1x1 shortcut draw (diffusion_utilities.py:54), on-device Philox.
+ * The stream id is sub (+ *sub_dev when given: a device counter advanced by cdm_counter_add, so a captured
+ * step draws fresh numbers on every replay). */
+int cdm_philox_normal(float* out, long long n, unsigned long long seed, unsigned int sub, const int* sub_dev,
+                      void* stream);
 int cdm_philox_uniform(float* out, long long n, float lo, float hi, unsigned long long seed, unsigned int sub,
+                       const int* sub_dev, void* stream);
+int cdm_philox_randint(int* out, int n, int lo, int hi, unsigned long long seed, unsigned int sub, const int* sub_dev,
                        void* stream);
-int cdm_philox_randint(int* out, int n, int lo, int hi, unsigned long long seed, unsigned int sub, void* stream);
+int cdm_counter_add(int* ctr, int delta, void* stream);
 /* torch.optim.Adam step (code/train_diffusion_condition.py:200,229); state = {lr, step, -, -} in device memory */
 int cdm_adam(float* p, const float* g, float* m, float* v, long long n, float* state, double beta1, double beta2,
-             double eps, void* stream);
+             double eps, float grad_scale, void* stream);
 /* weight repacking (+ eval-mode BatchNorm folding) */
 int cdm_pack_conv3x3(const float* W, const float* b, int Cin, int Cout, const float* gamma, const float* beta,
                      const float* rm, const float* rv, float eps, float* wpk, float* bpk, float* wdg, void* stream);
