@@ -219,17 +219,23 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_f32_kernel(LA la, LB lb, EP 
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     float4 ra[A_LD], rb[B_LD];
-    // per-thread fixed coordinates
+    // per-thread fixed coordinates (row / column decompositions hoisted out of the K loop)
     typename LB::Col bcol = lb.col(n0 + (tid % 32) * 4);
+    [[maybe_unused]] auto arows = [&]() {
+        if constexpr (!A_MCONTIG) {
+            struct Rows { typename LA::Row r[A_LD]; } rs;
+#pragma unroll
+            for (int i = 0; i < A_LD; ++i) rs.r[i] = la.row(m0 + tid / TPR + i * (GTHREADS / TPR));
+            return rs;
+        } else {
+            return 0;
+        }
+    }();
     auto gload = [&](int kt) {
         const int k0 = kt * BK;
         if constexpr (!A_MCONTIG) {
 #pragma unroll
-            for (int i = 0; i < A_LD; ++i) {
-                const int rr = tid / TPR + i * (GTHREADS / TPR);
-                const typename LA::Row row = la.row(m0 + rr);
-                ra[i] = la.load(row, k0 + (tid % TPR) * 4);
-            }
+            for (int i = 0; i < A_LD; ++i) ra[i] = la.load(arows.r[i], k0 + (tid % TPR) * 4);
         } else {
 #pragma unroll
             for (int i = 0; i < A_LD; ++i) ra[i] = la.loadT(k0 + tid / 32 + i * 8, m0 + (tid % 32) * 4);
@@ -324,19 +330,35 @@ static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); 
 // ---------------------------------------------------------------------------------------------
 // C ABI (declared in include/cdm_hip.h)
 // ---------------------------------------------------------------------------------------------
-CDM_API int cdm_conv3x3_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,
-                            const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
-                            void* stream) {
-    if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
+template <int BK>
+static int conv3x3_fwd_bk(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk, const float* bias,
+                          float* y, int ldy, int Cout, int flags, float* stats, int stats_ld, hipStream_t st) {
     const int M = N * H * W, K = 9 * Cin;
     LdDenseB lb{wpk, Cout, K, Cout};
     EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout};
     if (Cin == 128 && Cout == 128) {   // the 128-feature hot conv: its own (compile-time C) instantiation
         LdIm2colA<128> la{x, H, W, Cin, ldx, M, K};
-        return launch_gemm<LdIm2colA<128>, LdDenseB, EpiStore, false>(la, lb, ep, M, Cout, K, 1, S(stream));
+        return launch_gemm<LdIm2colA<128>, LdDenseB, EpiStore, false, BK>(la, lb, ep, M, Cout, K, 1, st);
     }
     LdIm2colA<0> la{x, H, W, Cin, ldx, M, K};
-    return launch_gemm<LdIm2colA<0>, LdDenseB, EpiStore, false>(la, lb, ep, M, Cout, K, 1, S(stream));
+    return launch_gemm<LdIm2colA<0>, LdDenseB, EpiStore, false, BK>(la, lb, ep, M, Cout, K, 1, st);
+}
+
+CDM_API int cdm_conv3x3_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,
+                            const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
+                            void* stream) {
+    if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
+    return conv3x3_fwd_bk<16>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, S(stream));
+}
+
+// tuning entry point: variant 0 = BK 16 (default), 1 = BK 32
+CDM_API int cdm_conv3x3_fwd_variant(int variant, const float* x, int N, int H, int W, int Cin, int ldx,
+                                    const float* wpk, const float* bias, float* y, int ldy, int Cout, int flags,
+                                    float* stats, int stats_ld, void* stream) {
+    if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
+    if (variant == 1)
+        return conv3x3_fwd_bk<32>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, S(stream));
+    return conv3x3_fwd_bk<16>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, S(stream));
 }
 
 CDM_API int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,

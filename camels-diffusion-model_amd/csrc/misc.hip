@@ -91,27 +91,32 @@ __global__ void philox_randint_kernel(int* out, int n, int lo, int hi, unsigned 
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void conv_cin1_fwd_kernel(const float* x, int N, int H, int W, const float* w9,
                                                             const float* bias, float* y, int ldy, int C, int relu) {
-    const int C4 = C >> 2;
-    const long long total = (long long)N * H * W * C4;
-    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (long long)gridDim.x * blockDim.x) {
-        const int c4 = (int)(idx % C4) * 4;
-        const long long pix = idx / C4;
+    // lanes span channels (one float4 each; a pixel's C channels are one coalesced row), the 9 input
+    // taps are wave-uniform broadcast loads, the 9x4 weights of a lane stay in registers.
+    const int C4 = C >> 2, PP = 256 / C4;
+    const int c4 = (threadIdx.x % C4) * 4, pl = threadIdx.x / C4;
+    if (pl >= PP) return;
+    float wr[9][4], bb[4];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wr[tap][j] = w9[tap * C + c4 + j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bb[j] = bias[c4 + j];
+    const long long P = (long long)N * H * W;
+    for (long long pix = (long long)blockIdx.x * PP + pl; pix < P; pix += (long long)gridDim.x * PP) {
         const int n = (int)(pix / (H * W)), rem = (int)(pix - (long long)n * H * W), h = rem / W, w = rem - h * W;
-        float xv[9];
+        float o[4] = {bb[0], bb[1], bb[2], bb[3]};
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
-            xv[tap] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? x[((long long)n * H + hh) * W + ww] : 0.f;
+            const float xv = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? x[((long long)n * H + hh) * W + ww] : 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = fmaf(xv, wr[tap][j], o[j]);
         }
-        float o[4];
+        if (relu) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            float s = 0.f;
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap) s = fmaf(xv[tap], w9[tap * C + c4 + j], s);
-            s += bias[c4 + j];
-            o[j] = relu ? fmaxf(s, 0.f) : s;
+            for (int j = 0; j < 4; ++j) o[j] = fmaxf(o[j], 0.f);
         }
         st4(y + pix * ldy + c4, make_float4(o[0], o[1], o[2], o[3]));
     }
@@ -154,14 +159,14 @@ __global__ __launch_bounds__(256) void conv_cin1_wgrad_kernel(const float* dy, i
     }
 }
 
-// out[r*s_r + c*s_c] (+)= sum_t slab[t][r0+r][c]  for r < rn
-__global__ void slab_sum_all_kernel(const float* slab, int ntiles, int R, int r0, int rn, int C, float* out,
+// out[r*s_r + c*s_c] (+)= sum_s part[s][r0+r][c]  for r < rn   (part = fp64 partials of cdm_slab_colsum)
+__global__ void slab_sum_all_kernel(const double* part, int S, int R, int r0, int rn, int C, float* out,
                                     long long s_r, long long s_c, int accumulate) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= rn * C) return;
     const int r = idx / C, c = idx - r * C;
     double s = 0.0;
-    for (int t = 0; t < ntiles; ++t) s += slab[((long long)t * R + r0 + r) * C + c];
+    for (int t = 0; t < S; ++t) s += part[((long long)t * R + r0 + r) * C + c];
     float* p = out + r * s_r + c * s_c;
     *p = accumulate ? *p + (float)s : (float)s;
 }
@@ -172,51 +177,63 @@ __global__ void slab_sum_all_kernel(const float* slab, int ntiles, int R, int r0
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void conv_cout1_fwd_kernel(const float* z, int ldz, int N, int H, int W, int C,
                                                              const float* w, const float* bias, float* out) {
-    extern __shared__ __attribute__((aligned(16))) float sh[];
-    float* ws = sh;                 // [9][C]  (tap-major)
-    float* part = sh + 9 * C;       // [4][64]
-    for (int i = threadIdx.x; i < 9 * C; i += 256) { const int tap = i / C, ci = i - tap * C; ws[i] = w[ci * 9 + tap]; }
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const long long pix = (long long)blockIdx.x * 64 + lane;
+    // lanes span channels (float4 each, coalesced 9 tap rows per pixel), per-lane 9x4 weights in
+    // registers, per-pixel dot product folded over the C/4 lanes through LDS.
+    __shared__ float part[256];
+    const int C4 = C >> 2, PP = 256 / C4;
+    const int c4 = (threadIdx.x % C4) * 4, pl = threadIdx.x / C4;
+    float wr[9][4];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wr[tap][j] = (pl < PP) ? w[(c4 + j) * 9 + tap] : 0.f;
     const long long P = (long long)N * H * W;
-    float s = 0.f;
-    if (pix < P) {
-        const int n = (int)(pix / (H * W)), rem = (int)(pix - (long long)n * H * W), h = rem / W, wx = rem - h * W;
-        for (int tap = 0; tap < 9; ++tap) {
-            const int hh = h + tap / 3 - 1, ww = wx + tap % 3 - 1;
-            if ((unsigned)hh >= (unsigned)H || (unsigned)ww >= (unsigned)W) continue;
-            const float* zp = z + (((long long)n * H + hh) * W + ww) * ldz;
-            const float* wt = ws + tap * C;
-            for (int c = wv * 4; c < C; c += 16) {
-                const float4 v = ld4(zp + c);
-                s = fmaf(v.x, wt[c], s); s = fmaf(v.y, wt[c + 1], s); s = fmaf(v.z, wt[c + 2], s); s = fmaf(v.w, wt[c + 3], s);
+    for (long long base = (long long)blockIdx.x * PP; base < P; base += (long long)gridDim.x * PP) {
+        const long long pix = base + pl;
+        float s = 0.f;
+        if (pl < PP && pix < P) {
+            const int n = (int)(pix / (H * W)), rem = (int)(pix - (long long)n * H * W), h = rem / W, wx = rem - h * W;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int hh = h + tap / 3 - 1, ww = wx + tap % 3 - 1;
+                if ((unsigned)hh >= (unsigned)H || (unsigned)ww >= (unsigned)W) continue;
+                const float4 v = ld4(z + (((long long)n * H + hh) * W + ww) * ldz + c4);
+                s = fmaf(v.x, wr[tap][0], s); s = fmaf(v.y, wr[tap][1], s);
+                s = fmaf(v.z, wr[tap][2], s); s = fmaf(v.w, wr[tap][3], s);
             }
         }
+        part[threadIdx.x] = s;
+        __syncthreads();
+        if (threadIdx.x < PP && base + threadIdx.x < P) {
+            float acc = bias[0];
+            for (int q = 0; q < C4; ++q) acc += part[threadIdx.x * C4 + q];
+            out[base + threadIdx.x] = acc;
+        }
+        __syncthreads();
     }
-    part[wv * 64 + lane] = s;
-    __syncthreads();
-    if (wv == 0 && pix < P) out[pix] = part[lane] + part[64 + lane] + part[128 + lane] + part[192 + lane] + bias[0];
 }
 
-// dz[p'][ci] = sum_tap deps[p' - tap + 1] * w[ci][tap]
+// dz[p'][ci] = sum_tap deps[p' - tap + 1] * w[ci][tap]   (lanes span channels, deps taps broadcast)
 __global__ __launch_bounds__(256) void conv_cout1_dgrad_kernel(const float* deps, int N, int H, int W, int C,
                                                                const float* w, float* dz, int lddz) {
-    const int C4 = C >> 2;
-    const long long total = (long long)N * H * W * C4;
-    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (long long)gridDim.x * blockDim.x) {
-        const int c4 = (int)(idx % C4) * 4;
-        const long long pix = idx / C4;
+    const int C4 = C >> 2, PP = 256 / C4;
+    const int c4 = (threadIdx.x % C4) * 4, pl = threadIdx.x / C4;
+    if (pl >= PP) return;
+    float wr[9][4];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wr[tap][j] = w[(c4 + j) * 9 + tap];
+    const long long P = (long long)N * H * W;
+    for (long long pix = (long long)blockIdx.x * PP + pl; pix < P; pix += (long long)gridDim.x * PP) {
         const int n = (int)(pix / (H * W)), rem = (int)(pix - (long long)n * H * W), h = rem / W, wx = rem - h * W;
         float o[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int hh = h - (tap / 3 - 1), ww = wx - (tap % 3 - 1);
-            if ((unsigned)hh >= (unsigned)H || (unsigned)ww >= (unsigned)W) continue;
-            const float g = deps[((long long)n * H + hh) * W + ww];
+            const float g = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? deps[((long long)n * H + hh) * W + ww] : 0.f;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = fmaf(g, w[(c4 + j) * 9 + tap], o[j]);
+            for (int j = 0; j < 4; ++j) o[j] = fmaf(g, wr[tap][j], o[j]);
         }
         st4(dz + pix * lddz + c4, make_float4(o[0], o[1], o[2], o[3]));
     }
@@ -544,8 +561,10 @@ CDM_API int cdm_philox_randint(int* out, int n, int lo, int hi, unsigned long lo
 CDM_API int cdm_conv3x3_cin1_fwd(const float* x, int N, int H, int W, const float* w9, const float* bias, float* y,
                                  int ldy, int C, int relu, void* stream) {
     if (C % 4) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(conv_cin1_fwd_kernel, dim3(nblocks((long long)N * H * W * (C / 4))), dim3(256), 0, S(stream), x, N,
-                       H, W, w9, bias, y, ldy, C, relu);
+    if (C > 1024) return (int)hipErrorInvalidValue;
+    const long long P = (long long)N * H * W;
+    hipLaunchKernelGGL(conv_cin1_fwd_kernel, dim3(nblocks(P, 256 / (C / 4), 4096)), dim3(256), 0, S(stream), x, N, H, W, w9,
+                       bias, y, ldy, C, relu);
     return cdm_status();
 }
 CDM_API int cdm_conv3x3_cin1_wgrad(const float* dy, int lddy, const float* x, int N, int H, int W, int C, int csize,
@@ -555,26 +574,26 @@ CDM_API int cdm_conv3x3_cin1_wgrad(const float* dy, int lddy, const float* x, in
                        H, W, C, csize, slab);
     return cdm_status();
 }
-CDM_API int cdm_slab_sum_all(const float* slab, int ntiles, int R, int r0, int rn, int C, float* out, long long s_r,
+CDM_API int cdm_slab_sum_all(const double* part, int nparts, int R, int r0, int rn, int C, float* out, long long s_r,
                              long long s_c, int accumulate, void* stream) {
-    hipLaunchKernelGGL(slab_sum_all_kernel, dim3((rn * C + 255) / 256), dim3(256), 0, S(stream), slab, ntiles, R, r0, rn, C,
+    hipLaunchKernelGGL(slab_sum_all_kernel, dim3((rn * C + 255) / 256), dim3(256), 0, S(stream), part, nparts, R, r0, rn, C,
                        out, s_r, s_c, accumulate);
     return cdm_status();
 }
 CDM_API int cdm_conv3x3_cout1_fwd(const float* z, int ldz, int N, int H, int W, int C, const float* w, const float* bias,
                                   float* out, void* stream) {
-    if (C % 4) return (int)hipErrorInvalidValue;
+    if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
     const long long P = (long long)N * H * W;
-    const size_t shm = (size_t)(9 * C + 256) * sizeof(float);
-    hipLaunchKernelGGL(conv_cout1_fwd_kernel, dim3((unsigned)((P + 63) / 64)), dim3(256), shm, S(stream), z, ldz, N, H, W,
-                       C, w, bias, out);
+    hipLaunchKernelGGL(conv_cout1_fwd_kernel, dim3(nblocks(P, 256 / (C / 4), 8192)), dim3(256), 0, S(stream), z, ldz, N, H,
+                       W, C, w, bias, out);
     return cdm_status();
 }
 CDM_API int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int C, const float* w, float* dz, int lddz,
                                     void* stream) {
-    if (C % 4) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(conv_cout1_dgrad_kernel, dim3(nblocks((long long)N * H * W * (C / 4))), dim3(256), 0, S(stream),
-                       deps, N, H, W, C, w, dz, lddz);
+    if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
+    const long long P = (long long)N * H * W;
+    hipLaunchKernelGGL(conv_cout1_dgrad_kernel, dim3(nblocks(P, 256 / (C / 4), 4096)), dim3(256), 0, S(stream), deps, N, H,
+                       W, C, w, dz, lddz);
     return cdm_status();
 }
 CDM_API int cdm_conv3x3_cout1_wgrad(const float* deps, const float* z, int ldz, int N, int H, int W, int C, int csize,

@@ -146,11 +146,33 @@ static int launch_reduce(const F& f, int N, int HWp, int C, int csize, float* sl
 }
 
 // -------------------------------------------------------------------------------------------------
-// finalize kernels (fp64 folding of the slabs)
+// stage 1 of every slab fold: part[s][r][c] = sum over tiles of split s of slab[t][r][c]   (fp64)
+// grid (ceil(C/64), S); 256 threads = 64 channels x 4 tile lanes (coalesced over channels)
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void slab_colsum_kernel(const float* __restrict__ slab, int ntiles, int R, int C,
+                                                          double* __restrict__ part, int per) {
+    __shared__ double red[4][64];
+    const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    const int t0 = blockIdx.y * per, t1 = min(ntiles, t0 + per);
+    for (int r = 0; r < R; ++r) {
+        double acc = 0.0;
+        if (c < C)
+            for (int t = t0 + lane; t < t1; t += 4) acc += (double)slab[((long long)t * R + r) * C + c];
+        red[lane][cl] = acc;
+        __syncthreads();
+        if (lane == 0 && c < C)
+            part[((long long)blockIdx.y * R + r) * C + c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+        __syncthreads();
+    }
+}
+
+// -------------------------------------------------------------------------------------------------
+// finalize kernels (fold the fp64 partials)
 // -------------------------------------------------------------------------------------------------
 // BatchNorm (train): per channel over all ntiles = N*nchunks partials.  Updates running stats like
 // torch (momentum 0.1, unbiased running var), increments num_batches_tracked (int64) once.
-__global__ void bn_fwd_finalize_kernel(const float* slab, int ntiles, int R, int C, double count,
+__global__ void bn_fwd_finalize_kernel(const double* part, int S, int R, int C, double count,
                                        const float* gamma, const float* beta, float* rmean, float* rvar,
                                        long long* nbt, float momentum, float eps, float* mean, float* invstd,
                                        float* scale, float* shift) {
@@ -158,9 +180,9 @@ __global__ void bn_fwd_finalize_kernel(const float* slab, int ntiles, int R, int
     if (c == 0 && nbt) *nbt += 1;
     if (c >= C) return;
     double s = 0.0, q = 0.0;
-    for (int t = 0; t < ntiles; ++t) {
-        s += slab[((long long)t * R + 0) * C + c];
-        q += slab[((long long)t * R + 1) * C + c];
+    for (int t = 0; t < S; ++t) {
+        s += part[((long long)t * R + 0) * C + c];
+        q += part[((long long)t * R + 1) * C + c];
     }
     const double mu = s / count;
     double var = q / count - mu * mu;
@@ -216,14 +238,14 @@ __global__ void gn_fwd_finalize_kernel(const float* slab, int nchunks, int R, in
 }
 
 // BatchNorm backward: dgamma/dbeta (assign), dy = A*gpre + B + Cc*xhat coefficients, conv bias grad.
-__global__ void bn_bwd_finalize_kernel(const float* slab, int ntiles, int C, double count, const float* gamma,
+__global__ void bn_bwd_finalize_kernel(const double* part, int S, int C, double count, const float* gamma,
                                        const float* invstd, float* dgamma, float* dbeta, float* A, float* B,
                                        float* Cc, float* dbias) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     double s1 = 0.0, s2 = 0.0, s5 = 0.0;
-    for (int t = 0; t < ntiles; ++t) {
-        const float* p = slab + (long long)t * 5 * C;
+    for (int t = 0; t < S; ++t) {
+        const double* p = part + (long long)t * 5 * C;
         s1 += p[0 * C + c]; s2 += p[1 * C + c]; s5 += p[4 * C + c];
     }
     const double a = (double)gamma[c] * (double)invstd[c];
@@ -428,10 +450,18 @@ CDM_API int cdm_norm_bwd_reduce(int mode, const float* g, int ldg, const float* 
     return launch_reduce(NormBwdF<false, false>{g, ldg, y, ldy, H, W, np, fp}, N, H * W, C, csize, slab, S(stream));
 }
 
-CDM_API int cdm_bn_fwd_finalize(const float* slab, int ntiles, int R, int C, double count, const float* gamma,
+CDM_API int cdm_slab_colsum(const float* slab, int ntiles, int R, int C, double* part, int splits, void* stream) {
+    if (splits < 1) splits = 1;
+    const int per = (ntiles + splits - 1) / splits;
+    hipLaunchKernelGGL(slab_colsum_kernel, dim3((C + 63) / 64, splits), dim3(256), 0, S(stream), slab, ntiles, R, C, part,
+                       per);
+    return cdm_status();
+}
+
+CDM_API int cdm_bn_fwd_finalize(const double* part, int nparts, int R, int C, double count, const float* gamma,
                                 const float* beta, float* rmean, float* rvar, long long* nbt, float momentum, float eps,
                                 float* mean, float* invstd, float* scale, float* shift, void* stream) {
-    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), slab, ntiles, R, C, count,
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), part, nparts, R, C, count,
                        gamma, beta, rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift);
     return cdm_status();
 }
@@ -452,10 +482,10 @@ CDM_API int cdm_gn_fwd_finalize(const float* slab, int N, int nchunks, int R, in
     return cdm_status();
 }
 
-CDM_API int cdm_bn_bwd_finalize(const float* slab, int ntiles, int C, double count, const float* gamma,
+CDM_API int cdm_bn_bwd_finalize(const double* part, int nparts, int C, double count, const float* gamma,
                                 const float* invstd, float* dgamma, float* dbeta, float* A, float* B, float* Cc,
                                 float* dbias, void* stream) {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), slab, ntiles, C, count,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), part, nparts, C, count,
                        gamma, invstd, dgamma, dbeta, A, B, Cc, dbias);
     return cdm_status();
 }

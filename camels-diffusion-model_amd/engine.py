@@ -257,7 +257,8 @@ class UNetEngine:
                                    l.cout, l.cout, 0, _p(ws.slab), l.cout, s)
                 ntiles = _cdiv(npix, CHUNK)
             bn = l.bn
-            lb.cdm_bn_fwd_finalize(_p(ws.slab), ntiles, 2, l.cout, float(npix), _p(P[bn + ".weight"]),
+            nparts = fold(ws, _p(ws.slab), ntiles, 2, l.cout, s)
+            lb.cdm_bn_fwd_finalize(_p(ws.dpart), nparts, 2, l.cout, float(npix), _p(P[bn + ".weight"]),
                                    _p(P[bn + ".bias"]), _p(P[bn + ".running_mean"]), _p(P[bn + ".running_var"]),
                                    _p(P[bn + ".num_batches_tracked"]), BN_MOM, BN_EPS, _p(st["mean"]),
                                    _p(st["invstd"]), _p(st["scale"]), _p(st["shift"]), s)
@@ -326,9 +327,10 @@ class UNetEngine:
         # ---------------- out.3 (nf -> 1) ----------------
         nch = _cdiv(H * H, CHUNK)
         lb.cdm_conv3x3_cout1_wgrad(_p(deps), _p(ws.zO), nf, B, H, H, nf, CHUNK, _p(ws.slab), s)
-        lb.cdm_slab_sum_all(_p(ws.slab), B * nch, 9, 0, 9, nf, _p(G["out.3.weight"]), 1, 9, 0, s)
+        S = fold(ws, _p(ws.slab), B * nch, 9, nf, s)
+        lb.cdm_slab_sum_all(_p(ws.dpart), S, 9, 0, 9, nf, _p(G["out.3.weight"]), 1, 9, 0, s)
         if not out3_bias_done:
-            _sum_into(deps, G["out.3.bias"], ws.slab, s)
+            _sum_into(deps, G["out.3.bias"], ws, s)
         gO = ws.G0
         lb.cdm_conv3x3_cout1_dgrad(_p(deps), B, H, H, nf, _p(P["out.3.weight"]), _p(gO), nf, s)
         # ---------------- out.1 GroupNorm + ReLU ----------------
@@ -411,7 +413,8 @@ class UNetEngine:
             lb.cdm_slab_sum_nc(_p(ws.slab), B, nch, 5, 3, C, _p(ws.d_emb["timeembed2"]), s)
         co = ws.coef
         bn = l.bn
-        lb.cdm_bn_bwd_finalize(_p(ws.slab), B * nch, C, float(B * S * S), _p(P[bn + ".weight"]), _p(st["invstd"]),
+        nparts = fold(ws, _p(ws.slab), B * nch, 5, C, s)
+        lb.cdm_bn_bwd_finalize(_p(ws.dpart), nparts, C, float(B * S * S), _p(P[bn + ".weight"]), _p(st["invstd"]),
                                _p(G[bn + ".weight"]), _p(G[bn + ".bias"]), _p(co[0]), _p(co[1]), _p(co[2]),
                                _p(G[l.b]), s)
         dy = ws.dy[l.name]
@@ -421,7 +424,8 @@ class UNetEngine:
         src = ws.src[l.name]
         if l.cin == 1:
             lb.cdm_conv3x3_cin1_wgrad(dy.p, dy.ld, _p(ws.x_in), B, S, S, C, CHUNK, _p(ws.slab), s)
-            lb.cdm_slab_sum_all(_p(ws.slab), B * _cdiv(S * S, CHUNK), 10, 0, 9, C, _p(G[l.w]), 1, 9, 0, s)
+            nparts = fold(ws, _p(ws.slab), B * _cdiv(S * S, CHUNK), 10, C, s)
+            lb.cdm_slab_sum_all(_p(ws.dpart), nparts, 10, 0, 9, C, _p(G[l.w]), 1, 9, 0, s)
             return
         self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s)
         dgd = ws.dgrad_dst[l.name]
@@ -440,7 +444,8 @@ class UNetEngine:
         lb = lib()
         Ho = 2 * Hin
         lb.cdm_reduce_sum(gy.p, gy.ld, B, Ho * Ho, cout, CHUNK, _p(ws.slab), s)
-        lb.cdm_slab_sum_all(_p(ws.slab), B * _cdiv(Ho * Ho, CHUNK), 1, 0, 1, cout, _p(G[name + ".bias"]), 0, 1, 0, s)
+        nparts = fold(ws, _p(ws.slab), B * _cdiv(Ho * Ho, CHUNK), 1, cout, s)
+        lb.cdm_slab_sum_all(_p(ws.dpart), nparts, 1, 0, 1, cout, _p(G[name + ".bias"]), 0, 1, 0, s)
         sp = wgrad_splits(B * Hin * Hin, cin, 4 * cout)
         lb.cdm_convT2x2_wgrad(x.p, B, Hin, Hin, cin, x.ld, gy.p, cout, gy.ld, sp, _p(ws.slab), s)
         # slab[z][ci][ij*cout+co] -> [ci][co][ij]
@@ -470,16 +475,25 @@ class UNetEngine:
                               _p(co[1]), _p(co[2]), C, dy.p, dy.ld, s)
 
 
-def _sum_into(x: torch.Tensor, out: torch.Tensor, scratch: torch.Tensor, stream: int):
+def _sum_into(x: torch.Tensor, out: torch.Tensor, ws, stream: int):
     """out[0] = sum(x) for a C=1 map: C=4 column partials over a [n/4, 4] view, then fold."""
     lb = lib()
     n = x.numel()
     assert n % 4 == 0
     nch = _cdiv(n // 4, CHUNK)
+    scratch = ws.slab
     lb.cdm_reduce_sum(_p(x), 4, 1, n // 4, 4, CHUNK, _p(scratch), stream)
     part = scratch[4 * nch: 4 * nch + 4]
-    lb.cdm_slab_sum_all(_p(scratch), nch, 1, 0, 1, 4, _p(part), 0, 1, 0, stream)
+    S = fold(ws, _p(scratch), nch, 1, 4, stream)
+    lb.cdm_slab_sum_all(_p(ws.dpart), S, 1, 0, 1, 4, _p(part), 0, 1, 0, stream)
     lb.cdm_col_sum(_p(part), 4, 1, _p(out), 0, stream)
+
+
+def fold(ws, slab_ptr: int, ntiles: int, R: int, C: int, stream: int) -> int:
+    """Stage-1 parallel fold of an fp32 partial slab [ntiles][R][C] into fp64 parts; returns #parts."""
+    S = max(1, min(ntiles, max(1, 512 // _cdiv(C, 64)), ws.dpart.numel() // max(1, R * C)))
+    lib().cdm_slab_colsum(slab_ptr, ntiles, R, C, _p(ws.dpart), S, stream)
+    return S
 
 
 def wgrad_splits(K: int, M: int, N: int) -> int:
@@ -568,6 +582,7 @@ class Workspace:
             else:
                 self.src[l.name] = self.dst[prev[l.name]]
         self.slab = E(self._slab_floats())
+        self.dpart = torch.empty(10 * 32768 + 4096, device=dev, dtype=torch.float64)
         self.sc_pending = None
         if train:
             C4 = 4 * nf

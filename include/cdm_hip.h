@@ -30,6 +30,10 @@ int cdm_device_sync(void);
  * per-128-pixel column sums / sums of squares (BatchNorm2d batch statistics, diffusion_utilities.py:28). */
 int cdm_conv3x3_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk, const float* bias,
                     float* y, int ldy, int Cout, int flags, float* stats, int stats_ld, void* stream);
+/* same, selecting a kernel variant (tuning: 0 = BK 16 default, 1 = BK 32) */
+int cdm_conv3x3_fwd_variant(int variant, const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,
+                            const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
+                            void* stream);
 /* nn.ConvTranspose2d(Cin,Cout,2,2) forward (diffusion_utilities.py:86); H,W = input grid. */
 int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk, const float* bias,
                      float* y, int ldy, int Cout, void* stream);
@@ -60,8 +64,10 @@ int cdm_reduce_sum(const float* g, int ldg, int N, int HW, int C, int csize, flo
 int cdm_norm_bwd_reduce(int mode, const float* g, int ldg, const float* y, int ldy, int N, int H, int W, int C,
                         const float* s, const float* t, int sn, const float* mean, const float* invstd, int mn,
                         int cpg, const float* film_a, int film_an, int csize, float* slab, void* stream);
+/* stage 1 of every slab fold: part[s][r][c] = sum_{tiles of split s} slab[t][r][c] in fp64 (parallel) */
+int cdm_slab_colsum(const float* slab, int ntiles, int R, int C, double* part, int splits, void* stream);
 /* BatchNorm2d train statistics + running-stat update (diffusion_utilities.py:28,35; momentum 0.1, eps 1e-5) */
-int cdm_bn_fwd_finalize(const float* slab, int ntiles, int R, int C, double count, const float* gamma,
+int cdm_bn_fwd_finalize(const double* part, int nparts, int R, int C, double count, const float* gamma,
                         const float* beta, float* rmean, float* rvar, long long* nbt, float momentum, float eps,
                         float* mean, float* invstd, float* scale, float* shift, void* stream);
 /* BatchNorm2d eval (running statistics) */
@@ -71,7 +77,7 @@ int cdm_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float
 int cdm_gn_fwd_finalize(const float* slab, int N, int nchunks, int R, int C, int G, double count, const float* gamma,
                         const float* beta, float eps, float* mean, float* invstd, float* scale, float* shift,
                         void* stream);
-int cdm_bn_bwd_finalize(const float* slab, int ntiles, int C, double count, const float* gamma, const float* invstd,
+int cdm_bn_bwd_finalize(const double* part, int nparts, int C, double count, const float* gamma, const float* invstd,
                         float* dgamma, float* dbeta, float* A, float* B, float* Cc, float* dbias, void* stream);
 int cdm_gn_bwd_finalize(const float* slab, int N, int nchunks, int C, int G, double count_g, int HW,
                         const float* gamma, const float* invstd, float* A, float* B, float* Cc, float* pdg, float* pdb,
@@ -94,7 +100,7 @@ int cdm_conv3x3_cin1_fwd(const float* x, int N, int H, int W, const float* wt, c
                          int C, int relu, void* stream);
 int cdm_conv3x3_cin1_wgrad(const float* dy, int lddy, const float* x, int N, int H, int W, int C, int csize,
                            float* slab, void* stream);
-int cdm_slab_sum_all(const float* slab, int ntiles, int R, int r0, int rn, int C, float* out, long long s_r,
+int cdm_slab_sum_all(const double* part, int nparts, int R, int r0, int rn, int C, float* out, long long s_r,
                      long long s_c, int accumulate, void* stream);
 /* out.3: Conv2d(nf, 1, 3, 1, 1) (ContextUnet.py:39) */
 int cdm_conv3x3_cout1_fwd(const float* z, int ldz, int N, int H, int W, int C, const float* w, const float* bias,
