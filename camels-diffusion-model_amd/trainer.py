@@ -155,6 +155,7 @@ class Trainer:
         self.use_graph = bool(use_graph) and not self.ddp
         self.graph = None
         self.steps = 0
+        self._inject = None
 
     # -------------------------------------------------------------------------------------------
     def P(self):
@@ -169,9 +170,14 @@ class Trainer:
         B, HW, nf = self.B, self.H * self.H, self.nf
         P = self._P
         seed = self.seed * 1000003 + (self._rank() << 20)
-        lb.cdm_philox_normal(_p(self.noise), B * HW, seed, 0, _p(self.ctr), s)
-        lb.cdm_philox_randint(_p(self.t_int), B, 1, self.T, seed, 1 << 24, _p(self.ctr), s)
-        lb.cdm_philox_uniform(_p(self.sc), 2 * nf, -1.0, 1.0, seed, 2 << 24, _p(self.ctr), s)
+        if self._inject is None:
+            lb.cdm_philox_normal(_p(self.noise), B * HW, seed, 0, _p(self.ctr), s)
+            lb.cdm_philox_randint(_p(self.t_int), B, 1, self.T, seed, 1 << 24, _p(self.ctr), s)
+            lb.cdm_philox_uniform(_p(self.sc), 2 * nf, -1.0, 1.0, seed, 2 << 24, _p(self.ctr), s)
+        else:                      # parity mode: caller-provided draws (eager only)
+            noise, t_int, sc = self._inject
+            self.noise.copy_(noise.reshape(-1)); self.t_int.copy_(t_int.reshape(-1))
+            self.sc.copy_(sc.reshape(-1))
         lb.cdm_perturb(_p(self.x0), _p(self.noise), _p(self.t_int), _p(self.sched.sab), _p(self.sched.omab), B, HW,
                        self.T, _p(self.xpert), _p(self.t_in), s)
         self.eng.repack(P, True, s)
@@ -200,8 +206,12 @@ class Trainer:
             self._body(torch.cuda.current_stream().cuda_stream)
         self.graph = g
 
-    def step(self, x0: Optional[torch.Tensor] = None, c: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """One training step on batch (x0 [B,1,H,H] in [0,1], c [B, n_cfeat] or None = unconditional)."""
+    def step(self, x0: Optional[torch.Tensor] = None, c: Optional[torch.Tensor] = None, inject=None) -> torch.Tensor:
+        """One training step on batch (x0 [B,1,H,H] in [0,1], c [B, n_cfeat] or None = unconditional).
+
+        ``inject=(noise [B,1,H,H], t [B] int, shortcut [2*n_feat] = weight|bias)`` replaces the on-device
+        Philox draws for this step (parity testing; runs eagerly)."""
+        self._inject = inject
         if x0 is not None:
             self.x0.copy_(x0.reshape(self.B, self.H, self.H))
         if c is not None:
@@ -210,7 +220,7 @@ class Trainer:
         if self.ddp and self.broadcast_buffers:
             import torch.distributed as dist
             dist.broadcast(self.bnflat, 0, group=self.group)
-        if self.use_graph:
+        if self.use_graph and inject is None:
             if self.graph is None:
                 self._body(_s())          # eager warm-up step (loads every kernel) then capture
                 self._capture()
