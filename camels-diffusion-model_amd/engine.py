@@ -155,6 +155,10 @@ class UNetEngine:
             self.pk[m + ".w2t"] = w2t
         self._pk_key = (key, train) if key is not None else None
 
+    def invalidate(self):
+        """Parameters changed behind torch's version counters (fused Adam): drop the cached eval pack."""
+        self._pk_key = None
+
     def _buf(self, name, shape):
         shape = (shape,) if isinstance(shape, int) else tuple(shape)
         t = self.pk.get(name)

@@ -136,28 +136,36 @@ class Trainer:
             self.bucketer = GradBucketer(self.gflat, self.ranges, group)
         # ---- optimizer state on device: [lr, step, -step_size, sqrt(bc2)] ----
         self.opt_state = torch.tensor([float(lrate), 0.0, 0.0, 1.0], device=dev)
-        # ---- step buffers ----
-        B, HW = self.B, self.H * self.H
+        # ---- step buffers (per batch size: the epoch's ragged last batch gets its own) ----
         self.sched = Schedule(self.T, dev)
-        self.x0 = torch.zeros(B, self.H, self.H, device=dev)
-        self.c = torch.zeros(B, self.ncf, device=dev)
-        self.noise = torch.empty(B * HW, device=dev)
-        self.t_int = torch.empty(B, dtype=torch.int32, device=dev)
-        self.t_in = torch.empty(B, device=dev)
-        self.xpert = torch.empty(B, self.H, self.H, device=dev)
         self.sc = torch.empty(2 * self.nf, device=dev)
-        self.deps = torch.empty(B, self.H, self.H, device=dev)
         self.nb = 256
         self.partial = torch.empty(2 * self.nb, device=dev)
         self.loss = torch.zeros(1, device=dev)
         self.ctr = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.ws = eng.workspace(B, True)
+        self._bufs: Dict[int, "_StepBufs"] = {}
+        self._use(self.B)
         self.use_graph = bool(use_graph) and not self.ddp
         self.graph = None
         self.steps = 0
         self._inject = None
 
     # -------------------------------------------------------------------------------------------
+    def _use(self, B: int):
+        b = self._bufs.get(B)
+        if b is None:
+            b = self._bufs[B] = _StepBufs(self.eng, B, self.H, self.ncf, self.dev)
+        self.cur = b
+        return b
+
+    @property
+    def x0(self):
+        return self.cur.x0
+
+    @property
+    def c(self):
+        return self.cur.c
+
     def P(self):
         _, P = self.model._engine_and_params()
         return P
@@ -167,25 +175,26 @@ class Trainer:
 
     def _body(self, s: int):
         lb = lib()
-        B, HW, nf = self.B, self.H * self.H, self.nf
+        sb = self.cur
+        B, HW, nf = sb.B, self.H * self.H, self.nf
         P = self._P
         seed = self.seed * 1000003 + (self._rank() << 20)
         if self._inject is None:
-            lb.cdm_philox_normal(_p(self.noise), B * HW, seed, 0, _p(self.ctr), s)
-            lb.cdm_philox_randint(_p(self.t_int), B, 1, self.T, seed, 1 << 24, _p(self.ctr), s)
+            lb.cdm_philox_normal(_p(sb.noise), B * HW, seed, 0, _p(self.ctr), s)
+            lb.cdm_philox_randint(_p(sb.t_int), B, 1, self.T, seed, 1 << 24, _p(self.ctr), s)
             lb.cdm_philox_uniform(_p(self.sc), 2 * nf, -1.0, 1.0, seed, 2 << 24, _p(self.ctr), s)
         else:                      # parity mode: caller-provided draws (eager only)
             noise, t_int, sc = self._inject
-            self.noise.copy_(noise.reshape(-1)); self.t_int.copy_(t_int.reshape(-1))
+            sb.noise.copy_(noise.reshape(-1)); sb.t_int.copy_(t_int.reshape(-1))
             self.sc.copy_(sc.reshape(-1))
-        lb.cdm_perturb(_p(self.x0), _p(self.noise), _p(self.t_int), _p(self.sched.sab), _p(self.sched.omab), B, HW,
-                       self.T, _p(self.xpert), _p(self.t_in), s)
+        lb.cdm_perturb(_p(sb.x0), _p(sb.noise), _p(sb.t_int), _p(self.sched.sab), _p(self.sched.omab), B, HW,
+                       self.T, _p(sb.xpert), _p(sb.t_in), s)
         self.eng.repack(P, True, s)
-        eps = self.eng.forward(self.ws, P, self.xpert, self.t_in, self.c, self.sc[:nf], self.sc[nf:], B, s)
-        lb.cdm_mse(_p(eps), _p(self.noise), B * HW, _p(self.deps), _p(self.partial), self.nb, _p(self.loss),
+        eps = self.eng.forward(sb.ws, P, sb.xpert, sb.t_in, sb.c, self.sc[:nf], self.sc[nf:], B, s)
+        lb.cdm_mse(_p(eps), _p(sb.noise), B * HW, _p(sb.deps), _p(self.partial), self.nb, _p(self.loss),
                    _p(self.grads["out.3.bias"]), s)
         hook = self.bucketer.stage_ready if self.ddp else None
-        self.eng.backward(self.ws, P, self.deps, self.grads, s, out3_bias_done=True, on_stage=hook)
+        self.eng.backward(sb.ws, P, sb.deps, self.grads, s, out3_bias_done=True, on_stage=hook)
         if self.ddp:
             self.bucketer.wait()
         lb.cdm_adam(_p(self.flat), _p(self.gflat), _p(self.m), _p(self.v), self.total, _p(self.opt_state), 0.9, 0.999,
@@ -212,15 +221,18 @@ class Trainer:
         ``inject=(noise [B,1,H,H], t [B] int, shortcut [2*n_feat] = weight|bias)`` replaces the on-device
         Philox draws for this step (parity testing; runs eagerly)."""
         self._inject = inject
+        B = self.B if x0 is None else x0.shape[0]
+        sb = self._use(B)
         if x0 is not None:
-            self.x0.copy_(x0.reshape(self.B, self.H, self.H))
+            sb.x0.copy_(x0.reshape(B, self.H, self.H))
         if c is not None:
-            self.c.copy_(c.reshape(self.B, self.ncf))
+            sb.c.copy_(c.reshape(B, self.ncf))
         self._P = self.P()
+        self.eng.invalidate()                 # the fused Adam updates parameters in place
         if self.ddp and self.broadcast_buffers:
             import torch.distributed as dist
             dist.broadcast(self.bnflat, 0, group=self.group)
-        if self.use_graph and inject is None:
+        if self.use_graph and inject is None and B == self.B:
             if self.graph is None:
                 self._body(_s())          # eager warm-up step (loads every kernel) then capture
                 self._capture()
@@ -230,3 +242,19 @@ class Trainer:
             self._body(_s())
         self.steps += 1
         return self.loss
+
+
+class _StepBufs:
+    """Device buffers of one training step at batch size B (engine workspace included)."""
+
+    def __init__(self, eng, B: int, H: int, ncf: int, dev):
+        HW = H * H
+        self.B = B
+        self.x0 = torch.zeros(B, H, H, device=dev)
+        self.c = torch.zeros(B, ncf, device=dev)
+        self.noise = torch.empty(B * HW, device=dev)
+        self.t_int = torch.empty(B, dtype=torch.int32, device=dev)
+        self.t_in = torch.empty(B, device=dev)
+        self.xpert = torch.empty(B, H, H, device=dev)
+        self.deps = torch.empty(B, H, H, device=dev)
+        self.ws = eng.workspace(B, True)

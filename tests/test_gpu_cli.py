@@ -1,0 +1,35 @@
+"""End-to-end CLI (train_diffusion.py LR EPOCHS T [NUM_PARAMS]) on synthetic maps, tiny config."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "camels-diffusion-model_amd", "train_diffusion.py")
+
+
+@pytest.mark.parametrize("args,cond", [(["1e-3", "2", "20", "6"], True), (["1e-3", "2", "20"], False)])
+def test_cli_trains_checkpoints_and_samples(tmp_path, args, cond):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    r = subprocess.run([sys.executable, CLI, *args, "--synthetic", "150", "--n-feat", "16", "--batch-size", "16",
+                        "--n-samples", "3", "--out-root", str(tmp_path)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    dirs = os.listdir(tmp_path)
+    assert len(dirs) == 1
+    out = tmp_path / dirs[0]
+    assert dirs[0].startswith("paper_lr_" if cond else "BIGnoiselr_")
+    loss = np.load(out / "loss_log.npy")
+    assert loss.shape == (2,) and np.isfinite(loss).all()
+    ckpts = os.listdir(out / "weights")
+    assert ckpts == (["model_epoch_2.pth"] if cond else [])
+    rec = np.load(out / "reconstructed_images.npy")
+    assert rec.shape == (3, 1, 64, 64) and np.isfinite(rec).all()
+    if cond:
+        sd = torch.load(out / "weights" / "model_epoch_2.pth", weights_only=True)
+        assert len(sd) == 156
+        assert np.load(out / "generated_samples.npy").shape == (3, 1, 64, 64)
