@@ -51,13 +51,13 @@ def time_dominant_conv(B: int, reps: int = 20):
     b = torch.zeros(NF, device="cuda")
     wpk = torch.empty(9 * NF, NF, device="cuda")
     L.cdm_pack_conv3x3(W.data_ptr(), b.data_ptr(), NF, NF, None, None, None, None, 0.0, wpk.data_ptr(), None, None,
-                       s.cuda_stream)
+                       16, s.cuda_stream)
     y = torch.empty(B * H * H, NF, device="cuda")
     stats = torch.empty((B * H * H + 127) // 128, 2, NF, device="cuda")
 
     def launch():
         L.cdm_conv3x3_fwd(x.data_ptr(), B, H, H, NF, NF, wpk.data_ptr(), b.data_ptr(), y.data_ptr(), NF, NF, 0,
-                          stats.data_ptr(), NF, s.cuda_stream)
+                          stats.data_ptr(), NF, 16, s.cuda_stream)
 
     for _ in range(3):
         launch()

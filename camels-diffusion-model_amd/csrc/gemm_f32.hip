@@ -34,8 +34,11 @@ struct LdDenseA {  // A[m][k] = a[m*lda + k]
     }
 };
 
-template <int CT>  // CT > 0: channel count known at compile time (the 128-feature hot conv)
-struct LdIm2colA {  // 3x3, stride 1, pad 1; m = (n,h,w), k = (ky*3+kx)*C + ci
+// K order: KC == 0 -> k = tap*C + ci (tap-major);  KC > 0 -> k = (cc*9 + tap)*KC + cj, ci = cc*KC + cj
+// (channel-chunk-major: the 9 taps of one KC-channel slab are consecutive K tiles, so they re-read the
+//  same ~17 KB input slab from L1/L2 instead of re-streaming the block's whole 131 KB input 9 times).
+template <int CT, int KC = 0>  // CT > 0: channel count known at compile time (the 128-feature hot conv)
+struct LdIm2colA {  // 3x3, stride 1, pad 1; m = (n,h,w)
     const float* x; int H, W, Crt, ldx, M, K;
     struct Row { int n, h, w; bool ok; };
     __device__ __forceinline__ Row row(int m) const {
@@ -45,7 +48,13 @@ struct LdIm2colA {  // 3x3, stride 1, pad 1; m = (n,h,w), k = (ky*3+kx)*C + ci
     __device__ __forceinline__ float4 load(const Row& r, int k) const {
         if (!r.ok || k >= K) return f4zero();
         const int C = CT > 0 ? CT : Crt;
-        const int tap = k / C, ci = k - tap * C;
+        int tap, ci;
+        if constexpr (KC > 0) {
+            const int cc = k / (9 * KC), rem = k - cc * 9 * KC;
+            tap = rem / KC; ci = cc * KC + (rem - tap * KC);
+        } else {
+            tap = k / C; ci = k - tap * C;
+        }
         const int ky = tap / 3, kx = tap - ky * 3;
         const int hh = r.h + ky - 1, ww = r.w + kx - 1;
         if ((unsigned)hh >= (unsigned)H || (unsigned)ww >= (unsigned)W) return f4zero();
@@ -167,7 +176,7 @@ struct EpiStore {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-t
         if (tid < GBN) {
             const int n = blockIdx.y * GBN + tid;
             if (n < N) {
-                float* st = stats + (long long)blockIdx.x * 2 * stats_ld;
+                float* st = stats + (long long)(mw / GBM) * 2 * stats_ld;
                 st[n] = scratch[0 * GBN + tid] + scratch[2 * GBN + tid];
                 st[stats_ld + n] = scratch[1 * GBN + tid] + scratch[3 * GBN + tid];
             }
@@ -192,7 +201,7 @@ struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n,
 };
 
 // ============================== the main loop ==============================
-template <class LA, class LB, class EP, bool A_MCONTIG, int BK>
+template <class LA, class LB, class EP, bool A_MCONTIG, int BK, bool XCD_REMAP = false>
 __global__ __launch_bounds__(GTHREADS, 2) void gemm_f32_kernel(LA la, LB lb, EP ep, int K, int kt_per_split) {
     constexpr int PADA = A_MCONTIG ? 4 : 2;   // k-major A image: stride == 2 (mod 32) -> conflict-free b32 transpose writes
     constexpr int SA = GBM + PADA, SB = GBN + 4;
@@ -205,7 +214,12 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_f32_kernel(LA la, LB lb, EP 
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    const int m0 = blockIdx.x * GBM, n0 = blockIdx.y * GBN;
+    int bx = blockIdx.x;
+    if constexpr (XCD_REMAP) {   // blocks b, b+8, ... share an XCD: give each XCD a contiguous run of M tiles
+        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = bx & 7, j = bx >> 3;
+        bx = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int m0 = bx * GBM, n0 = blockIdx.y * GBN;
     const int ktiles = (K + BK - 1) / BK;
     const int kt0 = blockIdx.z * kt_per_split;
     const int kt1 = min(ktiles, kt0 + kt_per_split);
@@ -282,7 +296,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_f32_kernel(LA la, LB lb, EP 
     ep(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, smem, tid);
 }
 
-template <class LA, class LB, class EP, bool A_MCONTIG, int BK = 16>
+template <class LA, class LB, class EP, bool A_MCONTIG, int BK = 16, bool XCD_REMAP = false>
 static int launch_gemm(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits, hipStream_t s) {
     const int ktiles = (K + BK - 1) / BK;
     if (splits < 1) splits = 1;
@@ -290,7 +304,8 @@ static int launch_gemm(const LA& la, const LB& lb, const EP& ep, int M, int N, i
     const int per = (ktiles + splits - 1) / splits;
     splits = ktiles > 0 ? (ktiles + per - 1) / per : 1;
     dim3 grid((M + GBM - 1) / GBM, (N + GBN - 1) / GBN, splits);
-    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, EP, A_MCONTIG, BK>), grid, dim3(GTHREADS), 0, s, la, lb, ep, K, per);
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, EP, A_MCONTIG, BK, XCD_REMAP>), grid, dim3(GTHREADS), 0, s, la, lb, ep, K,
+                       per);
     return cdm_status();
 }
 
@@ -330,35 +345,49 @@ static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); 
 // ---------------------------------------------------------------------------------------------
 // C ABI (declared in include/cdm_hip.h)
 // ---------------------------------------------------------------------------------------------
-template <int BK>
+template <int BK, int KC, bool XCD>
 static int conv3x3_fwd_bk(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk, const float* bias,
                           float* y, int ldy, int Cout, int flags, float* stats, int stats_ld, hipStream_t st) {
     const int M = N * H * W, K = 9 * Cin;
     LdDenseB lb{wpk, Cout, K, Cout};
     EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout};
     if (Cin == 128 && Cout == 128) {   // the 128-feature hot conv: its own (compile-time C) instantiation
-        LdIm2colA<128> la{x, H, W, Cin, ldx, M, K};
-        return launch_gemm<LdIm2colA<128>, LdDenseB, EpiStore, false, BK>(la, lb, ep, M, Cout, K, 1, st);
+        LdIm2colA<128, KC> la{x, H, W, Cin, ldx, M, K};
+        return launch_gemm<LdIm2colA<128, KC>, LdDenseB, EpiStore, false, BK, XCD>(la, lb, ep, M, Cout, K, 1, st);
     }
-    LdIm2colA<0> la{x, H, W, Cin, ldx, M, K};
-    return launch_gemm<LdIm2colA<0>, LdDenseB, EpiStore, false, BK>(la, lb, ep, M, Cout, K, 1, st);
+    LdIm2colA<0, KC> la{x, H, W, Cin, ldx, M, K};
+    return launch_gemm<LdIm2colA<0, KC>, LdDenseB, EpiStore, false, BK, XCD>(la, lb, ep, M, Cout, K, 1, st);
 }
 
+// kc = K order of the packed weights (cdm_pack_conv3x3): 16 = channel-chunk-major (needs Cin % 16 == 0),
+// 0 = tap-major.  Both run with the XCD-aware M-tile remap.
 CDM_API int cdm_conv3x3_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,
                             const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
-                            void* stream) {
-    if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
-    return conv3x3_fwd_bk<16>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, S(stream));
+                            int kc, void* stream) {
+    if (Cin % 4 || Cout % 4 || (kc != 0 && kc != 16) || (kc == 16 && Cin % 16)) return (int)hipErrorInvalidValue;
+    if (kc == 16)
+        return conv3x3_fwd_bk<16, 16, true>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld,
+                                            S(stream));
+    return conv3x3_fwd_bk<16, 0, true>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld,
+                                       S(stream));
 }
 
-// tuning entry point: variant 0 = BK 16 (default), 1 = BK 32
+// tuning entry point: 0 = default (BK16, tap-major K), 1 = BK32, 2 = XCD remap,
+// 3 = channel-chunk-major K (needs the kc=16 weight pack), 4 = 2 + 3
 CDM_API int cdm_conv3x3_fwd_variant(int variant, const float* x, int N, int H, int W, int Cin, int ldx,
                                     const float* wpk, const float* bias, float* y, int ldy, int Cout, int flags,
                                     float* stats, int stats_ld, void* stream) {
     if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
-    if (variant == 1)
-        return conv3x3_fwd_bk<32>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, S(stream));
-    return conv3x3_fwd_bk<16>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, S(stream));
+    hipStream_t st = S(stream);
+    switch (variant) {
+        case 1: return conv3x3_fwd_bk<32, 0, false>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, st);
+        case 2: return conv3x3_fwd_bk<16, 0, true>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, st);
+        case 3: if (Cin % 16) return (int)hipErrorInvalidValue;
+                return conv3x3_fwd_bk<16, 16, false>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, st);
+        case 4: if (Cin % 16) return (int)hipErrorInvalidValue;
+                return conv3x3_fwd_bk<16, 16, true>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, st);
+        default: return conv3x3_fwd_bk<16, 0, false>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, st);
+    }
 }
 
 CDM_API int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,

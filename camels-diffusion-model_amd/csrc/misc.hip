@@ -489,9 +489,15 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, long l
 // ------------------------------------------------------------------------------------------------
 // conv3x3 OIHW W[co][ci][tap] ->  wpk[(tap*Cin + ci)*Cout + co] (* fold[co]),  wdg[(tap*Cout+co)*Cin+ci] = W[co][ci][8-tap]
 // fold (eval BN): s = gamma/sqrt(rv+eps), bpk = (b - rm)*s + beta
+// kc > 0: channel-chunk-major K order k = ((ci/kc)*9 + tap)*kc + ci%kc  (must match LdIm2colA<.., KC>)
+static __device__ __forceinline__ long long kidx(int tap, int ci, int C, int kc) {
+    if (kc <= 0) return (long long)tap * C + ci;
+    const int cc = ci / kc;
+    return ((long long)cc * 9 + tap) * kc + (ci - cc * kc);
+}
 __global__ void pack_conv3x3_kernel(const float* W, const float* b, int Cin, int Cout, const float* gamma,
                                     const float* beta, const float* rm, const float* rv, float eps, float* wpk,
-                                    float* bpk, float* wdg) {
+                                    float* bpk, float* wdg, int kc) {
     const long long total = (long long)Cout * Cin * 9;
     for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
          idx += (long long)gridDim.x * blockDim.x) {
@@ -501,8 +507,8 @@ __global__ void pack_conv3x3_kernel(const float* W, const float* b, int Cin, int
         const float wv = W[idx];
         float s = 1.f;
         if (gamma) s = gamma[co] / sqrtf(rv[co] + eps);
-        if (wpk) wpk[((long long)tap * Cin + ci) * Cout + co] = wv * s;
-        if (wdg) wdg[((long long)(8 - tap) * Cout + co) * Cin + ci] = wv;
+        if (wpk) wpk[kidx(tap, ci, Cin, kc) * Cout + co] = wv * s;
+        if (wdg) wdg[kidx(8 - tap, co, Cout, kc) * Cin + ci] = wv;
         if (bpk && idx < Cout) {
             const int c = (int)idx;
             bpk[c] = gamma ? (b[c] - rm[c]) * (gamma[c] / sqrtf(rv[c] + eps)) + beta[c] : b[c];
@@ -667,10 +673,11 @@ CDM_API int cdm_adam(float* p, const float* g, float* m, float* v, long long n, 
     return cdm_status();
 }
 CDM_API int cdm_pack_conv3x3(const float* W, const float* b, int Cin, int Cout, const float* gamma, const float* beta,
-                             const float* rm, const float* rv, float eps, float* wpk, float* bpk, float* wdg,
+                             const float* rm, const float* rv, float eps, float* wpk, float* bpk, float* wdg, int kc,
                              void* stream) {
+    if (kc && ((wpk && Cin % kc) || (wdg && Cout % kc))) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(pack_conv3x3_kernel, dim3(nblocks((long long)Cout * Cin * 9)), dim3(256), 0, S(stream), W, b, Cin,
-                       Cout, gamma, beta, rm, rv, eps, wpk, bpk, wdg);
+                       Cout, gamma, beta, rm, rv, eps, wpk, bpk, wdg, kc);
     return cdm_status();
 }
 CDM_API int cdm_pack_convT(const float* W, int Cin, int Cout, int KK, float* wt, float* wtT, void* stream) {

@@ -69,6 +69,12 @@ class LayerSpec:
         self.name, self.cin, self.cout, self.S = name, cin, cout, S
         self.w, self.b = name + ".0.weight", name + ".0.bias"
         self.bn = name + ".1"
+        self.kc = conv_kc(cin, cout)
+
+
+def conv_kc(cin: int, cout: int) -> int:
+    """K order of a conv's packed weights: channel-chunk-major (16) when both channel counts allow."""
+    return 16 if (cin % 16 == 0 and cout % 16 == 0) else 0
 
 
 def conv_layers(nf: int, H: int):
@@ -100,6 +106,7 @@ class UNetEngine:
         self.layers = conv_layers(n_feat, height)
         self.L = {l.name: l for l in self.layers}
         self.KK0 = (height // 4) ** 2
+        self.kc_out0 = conv_kc(2 * n_feat, n_feat)
         self.pk: Dict[str, torch.Tensor] = {}
         self._pk_key = None
         self._ones = torch.ones(4 * n_feat, device=self.device)
@@ -118,7 +125,7 @@ class UNetEngine:
                 wpk = self._buf(l.name + ".wpk", (9 * l.cin, l.cout))
                 wdg = (self._buf(l.name + ".wdg", (9 * l.cout, l.cin))) if l.cin > 1 else None
                 lb.cdm_pack_conv3x3(_p(W), _p(b), l.cin, l.cout, None, None, None, None, 0.0, _p(wpk), None,
-                                    _p(wdg), stream)
+                                    _p(wdg), l.kc, stream)
                 self.pk[l.name + ".wpk"] = wpk
                 if wdg is not None:
                     self.pk[l.name + ".wdg"] = wdg
@@ -128,14 +135,14 @@ class UNetEngine:
                 bn = l.bn
                 lb.cdm_pack_conv3x3(_p(W), _p(b), l.cin, l.cout, _p(P[bn + ".weight"]), _p(P[bn + ".bias"]),
                                     _p(P[bn + ".running_mean"]), _p(P[bn + ".running_var"]), BN_EPS, _p(wpk),
-                                    _p(bpk), None, stream)
+                                    _p(bpk), None, l.kc, stream)
                 self.pk[l.name + ".wpk_e"] = wpk
                 self.pk[l.name + ".bpk_e"] = bpk
         # out.0 (GroupNorm follows: never folded)
         wpk = self._buf("out.0.wpk", (9 * 2 * nf, nf))
         wdg = self._buf("out.0.wdg", (9 * nf, 2 * nf))
         lb.cdm_pack_conv3x3(_p(P["out.0.weight"]), _p(P["out.0.bias"]), 2 * nf, nf, None, None, None, None, 0.0,
-                            _p(wpk), None, _p(wdg) if train else None, stream)
+                            _p(wpk), None, _p(wdg) if train else None, self.kc_out0, stream)
         self.pk["out.0.wpk"], self.pk["out.0.wdg"] = wpk, wdg
         for name, cin in (("up1.model.0", 4 * nf), ("up2.model.0", 2 * nf)):
             wt = self._buf(name + ".wt", (cin, 4 * nf))
@@ -236,7 +243,7 @@ class UNetEngine:
             self._conv_bn_fwd(ws, P, l, s, x)
         # ---------------- out ----------------
         lb.cdm_conv3x3_fwd(ws.catO.p, B, H, H, 2 * nf, 2 * nf, _p(self.pk["out.0.wpk"]), _p(P["out.0.bias"]),
-                           _p(ws.yO), nf, nf, 0, _p(ws.slab), nf, s)
+                           _p(ws.yO), nf, nf, 0, _p(ws.slab), nf, self.kc_out0, s)
         self._gn_fwd(ws, P, "out.1", Act(ws.yO, nf), B, H, nf, ws.gnO, stats_from_conv=True, stream=s)
         lb.cdm_norm_apply_fwd(APPLY_RELU, _p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]), _p(ws.gnO["shift"]), nf,
                               None, 0, None, 0, None, None, None, 0, _p(ws.zO), nf, s)
@@ -258,7 +265,7 @@ class UNetEngine:
                 ntiles = B * _cdiv(S * S, CHUNK)
             else:
                 lb.cdm_conv3x3_fwd(src.p, B, S, S, l.cin, src.ld, _p(self.pk[l.name + ".wpk"]), _p(P[l.b]), _p(y),
-                                   l.cout, l.cout, 0, _p(ws.slab), l.cout, s)
+                                   l.cout, l.cout, 0, _p(ws.slab), l.cout, l.kc, s)
                 ntiles = _cdiv(npix, CHUNK)
             bn = l.bn
             nparts = fold(ws, _p(ws.slab), ntiles, 2, l.cout, s)
@@ -276,7 +283,7 @@ class UNetEngine:
                                         _p(self.pk[l.name + ".bpk_e"]), outp.p, outp.ld, l.cout, 1, s)
             else:
                 lb.cdm_conv3x3_fwd(src.p, B, S, S, l.cin, src.ld, _p(self.pk[l.name + ".wpk_e"]),
-                                   _p(self.pk[l.name + ".bpk_e"]), outp.p, outp.ld, l.cout, EPI_RELU, None, 0, s)
+                                   _p(self.pk[l.name + ".bpk_e"]), outp.p, outp.ld, l.cout, EPI_RELU, None, 0, l.kc, s)
             if dense:
                 return
             scale, shift, relu = self._ones, self._zeros, 0
@@ -344,7 +351,7 @@ class UNetEngine:
         # ---------------- out.0 conv (2nf -> nf) ----------------
         self._wgrad3x3(ws, Act(dyO, nf), ws.catO, B, H, 2 * nf, nf, G["out.0.weight"], s)
         lb.cdm_conv3x3_fwd(_p(dyO), B, H, H, nf, nf, _p(self.pk["out.0.wdg"]), None, ws.dcatO.p, ws.dcatO.ld,
-                           2 * nf, 0, None, 0, s)
+                           2 * nf, 0, None, 0, self.kc_out0, s)
         hook("out")
         # ---------------- up2 blocks ----------------
         self._chain_bwd(ws, P, self.layers[14:18], G, s)
@@ -434,7 +441,7 @@ class UNetEngine:
         self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s)
         dgd = ws.dgrad_dst[l.name]
         lb.cdm_conv3x3_fwd(dy.p, B, S, S, C, dy.ld, _p(self.pk[l.name + ".wdg"]), None, dgd.p, dgd.ld, l.cin,
-                           EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, s)
+                           EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s)
 
     def _wgrad3x3(self, ws, dy: Act, x: Act, B, S, cin, cout, gW, s):
         lb = lib()

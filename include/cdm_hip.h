@@ -27,10 +27,11 @@ int cdm_device_sync(void);
 /* ---- contractions (fp32 MFMA 32x32x2; csrc/gemm_f32.hip) -------------------------------------- */
 /* nn.Conv2d(Cin,Cout,3,1,1) forward (diffusion_utilities.py:27,34; ContextUnet.py:36) and, with
  * flipped weights, its input gradient.  y (+)= conv(x) + bias; stats[tile][2][stats_ld] receives
- * per-128-pixel column sums / sums of squares (BatchNorm2d batch statistics, diffusion_utilities.py:28). */
+ * per-128-pixel column sums / sums of squares (BatchNorm2d batch statistics, diffusion_utilities.py:28).
+ * kc must equal the kc the weights were packed with (cdm_pack_conv3x3). */
 int cdm_conv3x3_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk, const float* bias,
-                    float* y, int ldy, int Cout, int flags, float* stats, int stats_ld, void* stream);
-/* same, selecting a kernel variant (tuning: 0 = BK 16 default, 1 = BK 32) */
+                    float* y, int ldy, int Cout, int flags, float* stats, int stats_ld, int kc, void* stream);
+/* same, selecting a kernel variant (tuning: 0 default, 1 BK32, 2 XCD remap, 3 chunked K, 4 = 2+3) */
 int cdm_conv3x3_fwd_variant(int variant, const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,
                             const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
                             void* stream);
@@ -142,8 +143,11 @@ int cdm_counter_add(int* ctr, int delta, void* stream);
 int cdm_adam(float* p, const float* g, float* m, float* v, long long n, float* state, double beta1, double beta2,
              double eps, float grad_scale, void* stream);
 /* weight repacking (+ eval-mode BatchNorm folding) */
+/* kc = 0: K order tap-major (k = tap*C + ci); kc = 16: channel-chunk-major (k = ((ci/16)*9 + tap)*16 + ci%16),
+ * the order cdm_conv3x3_fwd(kc = 16) consumes (wdg is chunked over Cout).  ConvTranspose packing: */
 int cdm_pack_conv3x3(const float* W, const float* b, int Cin, int Cout, const float* gamma, const float* beta,
-                     const float* rm, const float* rv, float eps, float* wpk, float* bpk, float* wdg, void* stream);
+                     const float* rm, const float* rv, float eps, float* wpk, float* bpk, float* wdg, int kc,
+                     void* stream);
 int cdm_pack_convT(const float* W, int Cin, int Cout, int KK, float* wt, float* wtT, void* stream);
 int cdm_transpose(const float* in, int R, int C, float* out, void* stream);
 

@@ -69,9 +69,13 @@ def test_bucketed_allreduce_equals_mean_of_shards(tmp_path):
     out = str(tmp_path / "flat.pt")
     mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     reduced = torch.load(out)
+    old = torch.get_num_threads()
     torch.set_num_threads(2)                 # same intra-op split as the workers: identical fp32 sums
-    m, g0 = _shard_grads(0)
-    _, g1 = _shard_grads(1)
+    try:
+        m, g0 = _shard_grads(0)
+        _, g1 = _shard_grads(1)
+    finally:
+        torch.set_num_threads(old)
     order = backward_order([n for n, _ in m.named_parameters()])
     expect = torch.cat([(g0[n] + g1[n]).reshape(-1) for _, grp in order for n in grp])
     err = (reduced - expect).abs().max().item()

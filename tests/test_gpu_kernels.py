@@ -36,16 +36,19 @@ def _nchw(y, N, H, W, C):
     return y.reshape(N, H, W, C).permute(0, 3, 1, 2).cpu()
 
 
-def _pack3x3(L, W, b, train=True):
+def _pack3x3(L, W, b, kc=0):
     Cout, Cin = W.shape[:2]
     wpk = torch.empty(9 * Cin, Cout, device="cuda"); wdg = torch.empty(9 * Cout, Cin, device="cuda")
     L.cdm_pack_conv3x3(W.data_ptr(), b.data_ptr(), Cin, Cout, None, None, None, None, 0.0, wpk.data_ptr(), None,
-                       wdg.data_ptr(), _s())
+                       wdg.data_ptr(), kc, _s())
     return wpk, wdg
 
 
+@pytest.mark.parametrize("kc", [0, 16])
 @pytest.mark.parametrize("N,H,Cin,Cout", [(2, 16, 32, 64), (1, 64, 128, 128), (3, 8, 8, 16), (2, 32, 256, 128)])
-def test_conv3x3_fwd_dgrad_wgrad(L, N, H, Cin, Cout):
+def test_conv3x3_fwd_dgrad_wgrad(L, N, H, Cin, Cout, kc):
+    if kc and (Cin % kc or Cout % kc):
+        pytest.skip("chunked K needs channels % 16 == 0")
     torch.manual_seed(0)
     x = torch.randn(N, Cin, H, H); W = torch.randn(Cout, Cin, 3, 3) * 0.1; b = torch.randn(Cout)
     gy = torch.randn(N, Cout, H, H)
@@ -53,13 +56,13 @@ def test_conv3x3_fwd_dgrad_wgrad(L, N, H, Cin, Cout):
     ref = F.conv2d(xg, Wg, bg, padding=1)
     ref.backward(gy)
     Wc, bc = W.cuda(), b.cuda()
-    wpk, wdg = _pack3x3(L, Wc, bc)
+    wpk, wdg = _pack3x3(L, Wc, bc, kc)
     xn = _nhwc(x)
     y = torch.empty(N * H * H, Cout, device="cuda")
     ntile = (N * H * H + 127) // 128
     stats = torch.zeros(ntile, 2, Cout, device="cuda")
     L.cdm_conv3x3_fwd(xn.data_ptr(), N, H, H, Cin, Cin, wpk.data_ptr(), bc.data_ptr(), y.data_ptr(), Cout, Cout, 0,
-                      stats.data_ptr(), Cout, _s())
+                      stats.data_ptr(), Cout, kc, _s())
     torch.cuda.synchronize()
     _close(_nchw(y, N, H, H, Cout), ref.detach())
     ysum = ref.detach().permute(0, 2, 3, 1).reshape(-1, Cout)
@@ -69,7 +72,7 @@ def test_conv3x3_fwd_dgrad_wgrad(L, N, H, Cin, Cout):
     gyn = _nhwc(gy)
     dx = torch.empty(N * H * H, Cin, device="cuda")
     L.cdm_conv3x3_fwd(gyn.data_ptr(), N, H, H, Cout, Cout, wdg.data_ptr(), None, dx.data_ptr(), Cin, Cin, 0, None, 0,
-                      _s())
+                      kc, _s())
     torch.cuda.synchronize()
     _close(_nchw(dx, N, H, H, Cin), xg.grad)
     # wgrad (split-K slabs) + reduce into OIHW
@@ -90,10 +93,10 @@ def test_conv3x3_channel_slices(L):
     big = torch.randn(N, H, H, 3 * Cin, device="cuda")
     x = big[..., Cin:2 * Cin]
     W = torch.randn(Cout, Cin, 3, 3, device="cuda") * 0.1; b = torch.randn(Cout, device="cuda")
-    wpk, _ = _pack3x3(L, W, b)
+    wpk, _ = _pack3x3(L, W, b, 16)
     out = torch.zeros(N, H, H, 2 * Cout, device="cuda")
     L.cdm_conv3x3_fwd(big.data_ptr() + 4 * Cin, N, H, H, Cin, 3 * Cin, wpk.data_ptr(), b.data_ptr(),
-                      out.data_ptr() + 4 * Cout, 2 * Cout, Cout, 1, None, 0, _s())
+                      out.data_ptr() + 4 * Cout, 2 * Cout, Cout, 1, None, 0, 16, _s())
     torch.cuda.synchronize()
     ref = F.relu(F.conv2d(x.permute(0, 3, 1, 2).cpu(), W.cpu(), b.cpu(), padding=1)).permute(0, 2, 3, 1)
     _close(out[..., Cout:], ref)

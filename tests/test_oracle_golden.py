@@ -10,7 +10,16 @@ import torch
 
 from oracle import ref_cpu as R
 
-torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+
+@pytest.fixture(autouse=True)
+def _eight_threads():
+    """The golden vectors were produced with 8 intra-op threads; CPU conv reductions are split per
+    thread, so bit-exactness holds at exactly that partitioning."""
+    old = torch.get_num_threads()
+    torch.set_num_threads(8)
+    yield
+    torch.set_num_threads(old)
 
 
 def _load(golden_dir, name):
