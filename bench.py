@@ -72,6 +72,18 @@ def time_dominant_conv(B: int, reps: int = 20):
     return ms, tflops
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes (tools/gpu_profile.sh:
+    FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected), or None when no profile has been collected."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_conv128.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return int(d["traffic_bytes"])
+
+
 def cpu_baseline(threads: int):
     """Reference algorithm (CPU oracle, torch CPU fp32) on a bounded sample of the same workload."""
     from oracle import ref_cpu as R
@@ -214,9 +226,9 @@ def main():
             "sample": {"img_per_s": round(sample_ips, 4), "T": T, "steps_run": S, "extrapolated": S < T,
                        "n_per_gpu": n, "guide_w": 0.0, "ms_per_denoise_step": round(dts / S * 1e3, 3),
                        "scaling": "replicas"},
-            "roofline": {"bound": "mfma", "kernel": "conv3x3 128->128 @64x64 fwd (gemm_f32_kernel<LdIm2colA<128>>)",
+            "roofline": {"bound": "mfma", "kernel": "conv3x3 128->128 @64x64 fwd (gemm_f32_kernel<LdIm2colA<128,16,64>>)",
                          "achieved": round(conv_tflops, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(conv_tflops / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                         "frac": round(conv_tflops / PEAK_FP32_TFLOPS, 4), "traffic": pmc_traffic(),
                          "launch_ms": round(conv_ms, 4),
                          "algorithmic": f"{CONV_GFLOP_PER_IMG} GFLOP/img x {B} img per launch"},
             "train_tflops_per_gpu": round(3 * FWD_GFLOP_PER_IMG * B / (ms_step * 1e-3) / 1e3, 2),

@@ -37,17 +37,19 @@ struct LdDenseA {  // A[m][k] = a[m*lda + k]
 // K order: KC == 0 -> k = tap*C + ci (tap-major);  KC > 0 -> k = (cc*9 + tap)*KC + cj, ci = cc*KC + cj
 // (channel-chunk-major: the 9 taps of one KC-channel slab are consecutive K tiles, so they re-read the
 //  same ~17 KB input slab from L1/L2 instead of re-streaming the block's whole 131 KB input 9 times).
-template <int CT, int KC = 0>  // CT > 0: channel count known at compile time (the 128-feature hot conv)
+template <int CT, int KC = 0, int HT = 0>  // CT/HT > 0: channels / square map size known at compile time
 struct LdIm2colA {  // 3x3, stride 1, pad 1; m = (n,h,w)
-    const float* x; int H, W, Crt, ldx, M, K;
+    const float* x; int Hrt, Wrt, Crt, ldx, M, K;
     struct Row { int n, h, w; bool ok; };
     __device__ __forceinline__ Row row(int m) const {
+        const int H = HT > 0 ? HT : Hrt, W = HT > 0 ? HT : Wrt;
         Row r; r.ok = m < M; const int hw = H * W; r.n = m / hw; const int rem = m - r.n * hw;
         r.h = rem / W; r.w = rem - r.h * W; return r;
     }
     __device__ __forceinline__ float4 load(const Row& r, int k) const {
         if (!r.ok || k >= K) return f4zero();
         const int C = CT > 0 ? CT : Crt;
+        const int H = HT > 0 ? HT : Hrt, W = HT > 0 ? HT : Wrt;
         int tap, ci;
         if constexpr (KC > 0) {
             const int cc = k / (9 * KC), rem = k - cc * 9 * KC;
@@ -351,7 +353,11 @@ static int conv3x3_fwd_bk(const float* x, int N, int H, int W, int Cin, int ldx,
     const int M = N * H * W, K = 9 * Cin;
     LdDenseB lb{wpk, Cout, K, Cout};
     EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout};
-    if (Cin == 128 && Cout == 128) {   // the 128-feature hot conv: its own (compile-time C) instantiation
+    if (Cin == 128 && Cout == 128 && H == 64 && W == 64) {   // the hot conv: own instantiation
+        LdIm2colA<128, KC, 64> la{x, H, W, Cin, ldx, M, K};
+        return launch_gemm<LdIm2colA<128, KC, 64>, LdDenseB, EpiStore, false, BK, XCD>(la, lb, ep, M, Cout, K, 1, st);
+    }
+    if (Cin == 128 && Cout == 128) {
         LdIm2colA<128, KC> la{x, H, W, Cin, ldx, M, K};
         return launch_gemm<LdIm2colA<128, KC>, LdDenseB, EpiStore, false, BK, XCD>(la, lb, ep, M, Cout, K, 1, st);
     }

@@ -8,7 +8,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(n=10, B=256, H=64, C=128, variant=0):
+def main(n=10, B=256, H=64, C=128, variant=-1):
     import cdm_amd
     L = cdm_amd.lib()
     s = torch.cuda.current_stream().cuda_stream
@@ -18,15 +18,19 @@ def main(n=10, B=256, H=64, C=128, variant=0):
     b = torch.zeros(C, device="cuda")
     wpk = torch.empty(9 * C, C, device="cuda")
     L.cdm_pack_conv3x3(W.data_ptr(), b.data_ptr(), C, C, None, None, None, None, 0.0, wpk.data_ptr(), None, None,
-                       16 if variant in (3, 4) else 0, s)
+                       16 if variant in (-1, 3, 4) else 0, s)
     y = torch.empty(B * H * H, C, device="cuda")
     st = torch.empty((B * H * H + 127) // 128, 2, C, device="cuda")
     for _ in range(n):
-        L.cdm_conv3x3_fwd_variant(variant, x.data_ptr(), B, H, H, C, C, wpk.data_ptr(), b.data_ptr(), y.data_ptr(), C,
-                                  C, 0, st.data_ptr(), C, s)
+        if variant < 0:    # the shipped path (engine / bench)
+            L.cdm_conv3x3_fwd(x.data_ptr(), B, H, H, C, C, wpk.data_ptr(), b.data_ptr(), y.data_ptr(), C, C, 0,
+                              st.data_ptr(), C, 16, s)
+        else:
+            L.cdm_conv3x3_fwd_variant(variant, x.data_ptr(), B, H, H, C, C, wpk.data_ptr(), b.data_ptr(),
+                                      y.data_ptr(), C, C, 0, st.data_ptr(), C, s)
     torch.cuda.synchronize()
     print("done", n)
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10, variant=int(sys.argv[2]) if len(sys.argv) > 2 else 0)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10, variant=int(sys.argv[2]) if len(sys.argv) > 2 else -1)
