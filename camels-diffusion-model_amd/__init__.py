@@ -6,8 +6,12 @@ repo-root ``cdm_amd.py`` shim maps the hyphenated directory to that name).
 """
 from ._lib import lib  # noqa: F401
 from .diffusion import DDPM, GraphSampler, Schedule, denoise_add_noise, perturb_input, sample_ddpm  # noqa: F401
+from .likelihood import (LikelihoodEvaluator, calculate_elbo_and_bpd, calculate_elbo_and_bpd_batch,  # noqa: F401
+                         calculate_elbo_and_bpd_dataset, calculate_likelihood)
 from .model import ContextUnet, EmbedFC, ResidualConvBlock, UnetDown, UnetUp  # noqa: F401
 from .trainer import Trainer  # noqa: F401
 
 __all__ = ["ContextUnet", "EmbedFC", "ResidualConvBlock", "UnetDown", "UnetUp", "lib", "DDPM", "GraphSampler",
-           "Schedule", "denoise_add_noise", "perturb_input", "sample_ddpm", "Trainer"]
+           "Schedule", "denoise_add_noise", "perturb_input", "sample_ddpm", "Trainer", "LikelihoodEvaluator",
+           "calculate_likelihood", "calculate_elbo_and_bpd", "calculate_elbo_and_bpd_batch",
+           "calculate_elbo_and_bpd_dataset"]

@@ -382,15 +382,44 @@ __global__ __launch_bounds__(256) void embed_bwd_param_kernel(Mlp4 P) {
 // diffusion elementwise math
 // ------------------------------------------------------------------------------------------------
 // x_pert = sqrt(ab[t]) x + (1 - ab[t]) noise ; temb_in = float(t)/float(T)
-__global__ void perturb_kernel(const float* x, const float* noise, const int* t, const float* sab, const float* omab,
-                               int N, int HW, float T, float* out, float* tin) {
+// t per sample (t != NULL) or one device-side step index (*cur_i) for the whole batch; in the latter case the
+// noise is row (T - i) of a table with row stride nstride (nstride = 0: a single noise buffer).
+// `omab` may be any noise-coefficient table (the paper ELBO uses sqrt(1 - ab)).
+__global__ void perturb_kernel(const float* x, const float* noise, const int* t, const int* cur_i, long long nstride,
+                               const float* sab, const float* omab, int N, int HW, int T, float* out, float* tin) {
 #pragma clang fp contract(off)  // keep the reference's separate fp32 roundings (bit-exact)
     const long long total = (long long)N * HW;
+    const int ci = cur_i ? *cur_i : 0;
+    const float* nz = cur_i ? noise + (long long)(T - ci) * nstride : noise;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
         const int n = (int)(i / HW);
-        const int ti = t[n];
-        out[i] = sab[ti] * x[i] + omab[ti] * noise[i];  // two roundings + one, as the reference (contract off)
-        if (tin && i - (long long)n * HW == 0) tin[n] = (float)ti / T;
+        const int ti = cur_i ? ci : t[n];
+        out[i] = sab[ti] * x[i] + omab[ti] * nz[i];
+        if (tin && i - (long long)n * HW == 0) tin[n] = (float)ti / (float)T;
+    }
+}
+
+// acc[n] += (mean_p (pred - noise)^2 * mul[i]) / div[i]   i = t[n] (per-sample steps) or *cur_i; one block per
+// sample, fixed reduction order (deterministic)
+// NLL term (code/train_diffusion_elbo.py:133-141): mul = 1, div = 2 b_t;  paper ELBO (:112-125): mul = w_t, div = 10
+__global__ __launch_bounds__(256) void mse_accum_kernel(const float* pred, const float* noise, long long nstride, int T,
+                                                        int HW, const int* t, const int* cur_i, const float* mul,
+                                                        const float* div, float* acc) {
+#pragma clang fp contract(off)
+    const int n = blockIdx.x, i = t ? t[n] : *cur_i;
+    const float* nz = t ? noise : noise + (long long)(T - i) * nstride;
+    float s = 0.f;
+    for (int p = threadIdx.x; p < HW; p += 256) {
+        const float d = pred[(long long)n * HW + p] - nz[(long long)n * HW + p];
+        s += d * d;
+    }
+    __shared__ float red[4];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float mse = (red[0] + red[1] + red[2] + red[3]) / (float)HW;
+        acc[n] += (mse * mul[i]) / div[i];
     }
 }
 
@@ -635,10 +664,18 @@ CDM_API int cdm_embed_bwd(const Mlp4* P, void* stream) {
     hipLaunchKernelGGL(embed_bwd_param_kernel, dim3(256, 4), dim3(256), 0, S(stream), *P);
     return cdm_status();
 }
-CDM_API int cdm_perturb(const float* x, const float* noise, const int* t, const float* sab, const float* omab, int N,
-                        int HW, int T, float* out, float* tin, void* stream) {
-    hipLaunchKernelGGL(perturb_kernel, dim3(nblocks((long long)N * HW)), dim3(256), 0, S(stream), x, noise, t, sab, omab, N,
-                       HW, (float)T, out, tin);
+CDM_API int cdm_perturb(const float* x, const float* noise, const int* t, const int* cur_i, long long nstride,
+                        const float* sab, const float* omab, int N, int HW, int T, float* out, float* tin, void* stream) {
+    if (!t && !cur_i) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(perturb_kernel, dim3(nblocks((long long)N * HW)), dim3(256), 0, S(stream), x, noise, t, cur_i,
+                       nstride, sab, omab, N, HW, T, out, tin);
+    return cdm_status();
+}
+CDM_API int cdm_mse_accum(const float* pred, const float* noise, long long nstride, int T, int N, int HW, const int* t,
+                          const int* cur_i, const float* mul, const float* div, float* acc, void* stream) {
+    if (!t && !cur_i) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(mse_accum_kernel, dim3(N), dim3(256), 0, S(stream), pred, noise, nstride, T, HW, t, cur_i, mul,
+                       div, acc);
     return cdm_status();
 }
 CDM_API int cdm_mse(const float* pred, const float* noise, long long n, float* dpred, float* partial, int nb,

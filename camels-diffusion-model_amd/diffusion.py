@@ -77,7 +77,7 @@ def perturb_input(x, t, noise, sched: Schedule):
     B = x.shape[0]
     out = torch.empty_like(x)
     ti = _as_i32(t, B, x.device)
-    lib().cdm_perturb(_p(x), _p(noise), _p(ti), _p(sched.sab), _p(sched.omab), B, x[0].numel(), sched.T,
+    lib().cdm_perturb(_p(x), _p(noise), _p(ti), None, 0, _p(sched.sab), _p(sched.omab), B, x[0].numel(), sched.T,
                       _p(out), None, _s())
     return out
 

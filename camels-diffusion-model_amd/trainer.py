@@ -187,7 +187,7 @@ class Trainer:
             noise, t_int, sc = self._inject
             sb.noise.copy_(noise.reshape(-1)); sb.t_int.copy_(t_int.reshape(-1))
             self.sc.copy_(sc.reshape(-1))
-        lb.cdm_perturb(_p(sb.x0), _p(sb.noise), _p(sb.t_int), _p(self.sched.sab), _p(self.sched.omab), B, HW,
+        lb.cdm_perturb(_p(sb.x0), _p(sb.noise), _p(sb.t_int), None, 0, _p(self.sched.sab), _p(self.sched.omab), B, HW,
                        self.T, _p(sb.xpert), _p(sb.t_in), s)
         self.eng.repack(P, True, s)
         eps = self.eng.forward(sb.ws, P, sb.xpert, sb.t_in, sb.c, self.sc[:nf], self.sc[nf:], B, s)

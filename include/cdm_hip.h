@@ -116,9 +116,15 @@ int cdm_avgpool_gelu_bwd(const float* dhv, const float* hpre, int N, int HW, int
 /* EmbedFC x4 (diffusion_utilities.py:118-145); `P` points to a host struct cdm_mlp4 (see csrc/misc.hip MlpDesc) */
 int cdm_embed_fwd(const void* P, void* stream);
 int cdm_embed_bwd(const void* P, void* stream);
-/* perturb_input (code/train_diffusion_condition.py:202-203) + t/T for the time embedding (:225) */
-int cdm_perturb(const float* x, const float* noise, const int* t, const float* sab, const float* omab, int N, int HW,
-                int T, float* out, float* tin, void* stream);
+/* perturb_input (code/train_diffusion_condition.py:202-203) + t/T for the time embedding (:225).
+ * t: per-sample steps, or cur_i: one device-side step for the batch with noise row (T - *cur_i)*nstride. */
+int cdm_perturb(const float* x, const float* noise, const int* t, const int* cur_i, long long nstride,
+                const float* sab, const float* omab, int N, int HW, int T, float* out, float* tin, void* stream);
+/* per-sample weighted MSE accumulation of the likelihood / ELBO estimators
+ * (code/train_diffusion_elbo.py:74-149; code/train_diffusion_paper.py:77-183):
+ * acc[n] += (mean (pred - noise)^2 * mul[i]) / div[i], i = t[n] or *cur_i (noise row (T - i)*nstride) */
+int cdm_mse_accum(const float* pred, const float* noise, long long nstride, int T, int N, int HW, const int* t,
+                  const int* cur_i, const float* mul, const float* div, float* acc, void* stream);
 /* F.mse_loss + its gradient (code/train_diffusion_condition.py:227) */
 int cdm_mse(const float* pred, const float* noise, long long n, float* dpred, float* partial, int nb, float* loss_out,
             float* dbias_out, void* stream);

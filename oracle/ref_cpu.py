@@ -21,6 +21,9 @@ Reference citations (paths relative to the reference repo root):
   UnetUp / UnetDown   code/diffusion_utilities.py:79-116
   EmbedFC             code/diffusion_utilities.py:118-145
   train step          code/train_diffusion_condition.py:206-232 (Adam :200, LR decay :213)
+  likelihood (NLL)    code/train_diffusion_elbo.py:108-149 (== code/train_diffusion_paper.py:142-183)
+  ELBO/BPD, dataset   code/train_diffusion_paper.py:77-139
+  ELBO/BPD, per batch code/train_diffusion_elbo.py:74-105
 """
 from __future__ import annotations
 
@@ -306,6 +309,58 @@ def make_model_fn(sd, *, n_feat, n_cfeat, height, train=False, shortcut_log=None
             return unet_forward(sd, x, t, c, n_feat=n_feat, n_cfeat=n_cfeat, height=height,
                                 train=train, shortcut=draw)
     return fn
+
+
+# ----------------------------------------------------------------------------------------------
+# next-1: likelihood / ELBO estimators (model(x, t, c) as from make_model_fn, eval mode)
+def calculate_likelihood(model: Callable, batches, timesteps: int, sched) -> float:
+    """code/train_diffusion_elbo.py:108-149: sum_t mse_t / (2 b_t) per sample, t = 1..T ascending,
+    x_t = sqrt(ab) x + (1 - ab) noise (same non-standard factor as perturb_input); noise ~ randn_like
+    (CPU RNG, drawn before the model call, whose shortcut draw follows)."""
+    b_t, a_t, ab_t = sched
+    total, count = 0.0, 0
+    for x, param in batches:
+        bsz = x.shape[0]
+        acc = torch.zeros(bsz)
+        for t in range(1, timesteps + 1):
+            noise = torch.randn_like(x)
+            x_t = ab_t.sqrt()[t, None, None, None] * x + (1 - ab_t[t, None, None, None]) * noise
+            pred = model(x_t, torch.tensor([t / timesteps]), param)
+            mse = F.mse_loss(pred, noise, reduction="none").mean(dim=[1, 2, 3])
+            acc += mse / (2 * b_t[t])
+        total += acc.sum().item()
+        count += bsz
+    return total / count
+
+
+def calculate_elbo_and_bpd_dataset(model: Callable, batches, timesteps: int, sched):
+    """code/train_diffusion_paper.py:77-139: 10 evenly spaced t (linspace(1,T,10).long()), standard
+    sqrt(1 - ab) noise factor, weight 0.5 b/(1 - ab) for t > 1, /10; bpd over 64*64 dims."""
+    b_t, a_t, ab_t = sched
+    total, count = 0.0, 0
+    for x, param in batches:
+        bsz = x.shape[0]
+        acc = torch.zeros(bsz)
+        for t in torch.linspace(1, timesteps, 10).long():
+            noise = torch.randn_like(x)
+            x_t = ab_t.sqrt()[t] * x + torch.sqrt(1 - ab_t[t]) * noise
+            pred = model(x_t, torch.tensor([t / timesteps]), param)
+            mse = F.mse_loss(pred, noise, reduction="none").mean(dim=[1, 2, 3])
+            if t > 1:
+                w = 0.5 * (b_t[t] / (1.0 - ab_t[t]))
+                acc += w * mse / 10.0
+        total += acc.sum().item()
+        count += bsz
+    avg = total / count
+    return avg, avg / (64 * 64 * math.log(2))
+
+
+def calculate_elbo_and_bpd_batch(x, pred_noise, noise, t, b_t, a_t, ab_t, dims):
+    """code/train_diffusion_elbo.py:74-105 (per training batch, per-sample t)."""
+    mse = F.mse_loss(pred_noise, noise, reduction="none").mean(dim=[1, 2, 3])
+    w = 0.5 * (1.0 / (1.0 - ab_t[t]) - 1.0)
+    elbo = (w * mse).mean()
+    return elbo, elbo / (dims * math.log(2))
 
 
 def forward_flops(n_feat: int, height: int, in_channels: int = 1, n_cfeat: int = 6) -> float:

@@ -7,6 +7,7 @@ What it does (and why each piece is legitimate test data, not copied source):
     ``torchvision`` stub (torchvision is absent here and none of its symbols is on the hot path:
     diffusion_utilities.py:4,8 import save_image/make_grid/transforms at module level only);
   * AST-lifts ``perturb_input``, ``denoise_add_noise``, ``sample_ddpm``, ``sample_ddpm_from_noise``
+    (and ``calculate_likelihood`` / ``calculate_elbo_and_bpd`` from the elbo and paper scripts)
     out of ``code/train_diffusion_condition.py`` (that script runs training at import time, so it
     cannot be imported) and executes them in a namespace that supplies the globals they read;
   * runs them on seeded synthetic inputs (trained weights / CAMELS maps are Git-LFS stubs, F9)
@@ -182,6 +183,43 @@ def main():
               fromnoise_out=xs.numpy(), fromnoise_inter=inter)
     fx["T"] = np.array(T_SAMPLE)
     np.savez_compressed(os.path.join(OUT, "sampler_nf8.npz"), **fx)
+
+    # ---------------- likelihood / ELBO estimators (next-1), CPU RNG order ----------------
+    # calculate_likelihood (code/train_diffusion_elbo.py:108-149), calculate_elbo_and_bpd dataset form
+    # (code/train_diffusion_paper.py:77-139) and per-batch form (code/train_diffusion_elbo.py:74-105)
+    elbo_script = os.path.join(REF, "code", "train_diffusion_elbo.py")
+    paper_script = os.path.join(REF, "code", "train_diffusion_paper.py")
+    fx = {}
+    gl = torch.Generator().manual_seed(90)
+    batches = [(torch.rand(2, 1, 64, 64, generator=gl), torch.rand(2, ncf, generator=gl)),
+               (torch.rand(1, 1, 64, 64, generator=gl), torch.rand(1, ncf, generator=gl))]  # ragged last batch
+    for j, (xb, pb) in enumerate(batches):
+        fx[f"lik_x{j}"], fx[f"lik_c{j}"] = xb.numpy(), pb.numpy()
+    ns_e = {"torch": torch, "np": np, "F": F}
+    _lift(elbo_script, ["calculate_likelihood", "calculate_elbo_and_bpd"], ns_e)
+    ns_p = {"torch": torch, "np": np, "F": F}
+    _lift(paper_script, ["calculate_likelihood", "calculate_elbo_and_bpd"], ns_p)
+    T_LIK = 10
+    b_t, a_t, ab_t = sched(T_LIK)
+    torch.manual_seed(600)
+    fx["nll_elbo_script"] = np.array(ns_e["calculate_likelihood"](model, batches, T_LIK, "cpu", ab_t, b_t, a_t))
+    torch.manual_seed(600)
+    fx["nll_paper_script"] = np.array(ns_p["calculate_likelihood"](model, batches, T_LIK, "cpu", ab_t, b_t, a_t))
+    T_ELBO = 1500
+    b_t, a_t, ab_t = sched(T_ELBO)
+    torch.manual_seed(601)
+    elbo, bpd = ns_p["calculate_elbo_and_bpd"](model, batches, T_ELBO, "cpu", ab_t, b_t, a_t)
+    fx["paper_elbo"], fx["paper_bpd"] = np.array(elbo), np.array(bpd)
+    # per-batch form on a (x, pred_noise, noise, t) quadruple
+    ge = torch.Generator().manual_seed(91)
+    xq = torch.rand(5, 1, 64, 64, generator=ge); pq = torch.randn(5, 1, 64, 64, generator=ge)
+    nq = torch.randn(5, 1, 64, 64, generator=ge); tq = torch.randint(1, T_ELBO + 1, (5,), generator=ge)
+    e, bp = ns_e["calculate_elbo_and_bpd"](xq, pq, nq, tq, b_t, a_t, ab_t, 64 * 64)
+    fx.update(batch_x=xq.numpy(), batch_pred=pq.numpy(), batch_noise=nq.numpy(), batch_t=tq.numpy(),
+              batch_elbo=e.numpy(), batch_bpd=bp.numpy())
+    fx["T_lik"], fx["T_elbo"] = np.array(T_LIK), np.array(T_ELBO)
+    np.savez_compressed(os.path.join(OUT, "likelihood_nf8.npz"), **fx)
+    print("likelihood:", {k: float(v) for k, v in fx.items() if v.ndim == 0})
 
     # ---------------- layout metadata at the bench config ----------------
     torch.manual_seed(0)

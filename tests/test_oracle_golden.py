@@ -140,3 +140,31 @@ def test_sampler_random_params_and_from_noise(golden_dir):
 
 def test_forward_flops_matches_survey():
     assert abs(R.forward_flops(128, 64) / 1e9 - 19.178788) < 2e-3
+
+
+def _lik_batches(lfx):
+    return [(torch.from_numpy(lfx[f"lik_x{j}"]), torch.from_numpy(lfx[f"lik_c{j}"])) for j in range(2)]
+
+
+def test_likelihood_and_elbo_bit_exact(golden_dir):
+    """next-1: the NLL estimator (both scripts) and the dataset ELBO/BPD, CPU RNG order."""
+    lfx = _load(golden_dir, "likelihood_nf8.npz")
+    sd = _sd(_load(golden_dir, "model_nf8.npz"))
+    fn = R.make_model_fn(sd, n_feat=8, n_cfeat=6, height=64)
+    T = int(lfx["T_lik"])
+    torch.manual_seed(600)
+    nll = R.calculate_likelihood(fn, _lik_batches(lfx), T, R.make_schedule(T))
+    assert nll == float(lfx["nll_elbo_script"]) == float(lfx["nll_paper_script"])
+    T = int(lfx["T_elbo"])
+    torch.manual_seed(601)
+    elbo, bpd = R.calculate_elbo_and_bpd_dataset(fn, _lik_batches(lfx), T, R.make_schedule(T))
+    assert elbo == float(lfx["paper_elbo"]) and bpd == float(lfx["paper_bpd"])
+
+
+def test_batch_elbo_bit_exact(golden_dir):
+    lfx = _load(golden_dir, "likelihood_nf8.npz")
+    b, a, ab = R.make_schedule(int(lfx["T_elbo"]))
+    g = lambda k: torch.from_numpy(lfx[k])
+    e, bp = R.calculate_elbo_and_bpd_batch(g("batch_x"), g("batch_pred"), g("batch_noise"), g("batch_t"), b, a, ab,
+                                           64 * 64)
+    assert e.item() == float(lfx["batch_elbo"]) and bp.item() == float(lfx["batch_bpd"])
