@@ -31,6 +31,11 @@ NF, NCF, H, T = 128, 6, 64, 1500
 CONV_GFLOP_PER_IMG = 1.2079596          # conv3x3 128->128 @ 64x64
 FWD_GFLOP_PER_IMG = 19.178788
 PEAK_FP32_TFLOPS = 157.3                # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+PEAK_BF16_TFLOPS = 2500.0               # MI355X dense bf16 MFMA (no sparsity)
+# conv arithmetic -> (bf16 MFMA products per fp32 MAC, description); peak = fp32-equivalent FLOP/s ceiling
+CONV_MATH_INFO = {"fp32": (0, "fp32 MFMA v_mfma_f32_32x32x2_f32"),
+                  "x6": (6, "fp32-accurate split-bf16: 3-term bf16 operands, 6 cross products on "
+                            "v_mfma_f32_32x32x16_bf16, fp32 accumulate")}
 
 
 def _dist_env():
@@ -40,7 +45,12 @@ def _dist_env():
     return ws, rank, local
 
 
-def time_dominant_conv(B: int, reps: int = 20):
+def conv_peak(math: str) -> float:
+    nprod = CONV_MATH_INFO[math][0]
+    return PEAK_FP32_TFLOPS if nprod == 0 else PEAK_BF16_TFLOPS / nprod
+
+
+def time_dominant_conv(B: int, math: str, reps: int = 20):
     """Average duration of the conv3x3 128->128 @64x64 kernel (HIP events on its own stream)."""
     import cdm_amd
     L = cdm_amd.lib()
@@ -54,10 +64,17 @@ def time_dominant_conv(B: int, reps: int = 20):
                        16, s.cuda_stream)
     y = torch.empty(B * H * H, NF, device="cuda")
     stats = torch.empty((B * H * H + 127) // 128, 2, NF, device="cuda")
+    nterm = CONV_MATH_INFO[math][0]
+    wx = torch.empty(9 * NF // 16 * 3 * NF * 16, dtype=torch.bfloat16, device="cuda")
+    L.cdm_split_bf16x3(wpk.data_ptr(), NF, 9 * NF, NF, wx.data_ptr(), s.cuda_stream)
 
     def launch():
-        L.cdm_conv3x3_fwd(x.data_ptr(), B, H, H, NF, NF, wpk.data_ptr(), b.data_ptr(), y.data_ptr(), NF, NF, 0,
-                          stats.data_ptr(), NF, 16, s.cuda_stream)
+        if nterm:
+            L.cdm_conv3x3_fwd_x3(x.data_ptr(), B, H, H, NF, NF, wx.data_ptr(), b.data_ptr(), y.data_ptr(), NF, NF, 0,
+                                 stats.data_ptr(), NF, 16, nterm, s.cuda_stream)
+        else:
+            L.cdm_conv3x3_fwd(x.data_ptr(), B, H, H, NF, NF, wpk.data_ptr(), b.data_ptr(), y.data_ptr(), NF, NF, 0,
+                              stats.data_ptr(), NF, 16, s.cuda_stream)
 
     for _ in range(3):
         launch()
@@ -72,11 +89,12 @@ def time_dominant_conv(B: int, reps: int = 20):
     return ms, tflops
 
 
-def pmc_traffic():
+def pmc_traffic(math: str):
     """HBM bytes per launch of the dominant kernel from the committed PMC passes (tools/gpu_profile.sh:
     FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected), or None when no profile has been collected."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_conv128.json")))
+    suffix = "" if math == "fp32" else "_" + math
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_conv128{suffix}.json")))
     if not files:
         return None
     with open(files[-1]) as f:
@@ -139,6 +157,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--conv-math", choices=sorted(CONV_MATH_INFO), default="x6",
+                    help="3x3 conv arithmetic (both fp32-accurate; see DESIGN.md §3)")
     args = ap.parse_args()
 
     world, rank, local = _dist_env()
@@ -153,7 +173,7 @@ def main():
 
     B = args.batch
     torch.manual_seed(0)
-    model = ContextUnet(1, NF, NCF, H, shortcut_source="device").cuda()
+    model = ContextUnet(1, NF, NCF, H, shortcut_source="device", conv_math=args.conv_math).cuda()
     trainer = Trainer(model, 1e-5, T, B, seed=rank, use_graph=not args.no_graph)
     g = torch.Generator(device="cuda").manual_seed(1234 + rank)
     x0 = torch.rand(B, 1, H, H, device="cuda", generator=g)   # synthetic maps in [0,1) (min-max range)
@@ -202,7 +222,8 @@ def main():
     sample_ips = world * n / (dts * T / S)
 
     # ---------------- roofline of the dominant kernel ----------------
-    conv_ms, conv_tflops = time_dominant_conv(B)
+    conv_ms, conv_tflops = time_dominant_conv(B, args.conv_math)
+    peak = conv_peak(args.conv_math)
 
     out = None
     if rank == 0:
@@ -222,15 +243,23 @@ def main():
             "config": {"workload": "ContextUnet DDPM train step (fwd+bwd+Adam), n_feat=128, 6 params, 64x64x1, "
                                    "T=1500, train-mode BatchNorm",
                        "batch_per_gpu": B, "global_batch": B * world, "n_feat": NF, "n_cfeat": NCF, "T": T,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "conv_math": args.conv_math},
             "sample": {"img_per_s": round(sample_ips, 4), "T": T, "steps_run": S, "extrapolated": S < T,
                        "n_per_gpu": n, "guide_w": 0.0, "ms_per_denoise_step": round(dts / S * 1e3, 3),
                        "scaling": "replicas"},
-            "roofline": {"bound": "mfma", "kernel": "conv3x3 128->128 @64x64 fwd (gemm_f32_kernel<LdIm2colA<128,16,64>>)",
-                         "achieved": round(conv_tflops, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(conv_tflops / PEAK_FP32_TFLOPS, 4), "traffic": pmc_traffic(),
+            "roofline": {"bound": "mfma",
+                         "kernel": "conv3x3 128->128 @64x64 fwd (" + ("gemm_x3_kernel<StageRowK<LdIm2colA<128,16,64>>,"
+                                   "StagePre>" if CONV_MATH_INFO[args.conv_math][0] else
+                                   "gemm_f32_kernel<LdIm2colA<128,16,64>>") + ")",
+                         "arithmetic": CONV_MATH_INFO[args.conv_math][1],
+                         "achieved": round(conv_tflops, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
+                         "frac": round(conv_tflops / peak, 4), "traffic": pmc_traffic(args.conv_math),
                          "launch_ms": round(conv_ms, 4),
-                         "algorithmic": f"{CONV_GFLOP_PER_IMG} GFLOP/img x {B} img per launch"},
+                         "algorithmic": f"{CONV_GFLOP_PER_IMG} GFLOP/img x {B} img per launch (fp32 FLOPs); peak = "
+                                        + ("fp32 MFMA dense" if peak == PEAK_FP32_TFLOPS else
+                                           f"bf16 MFMA dense {PEAK_BF16_TFLOPS:.0f} / "
+                                           f"{CONV_MATH_INFO[args.conv_math][0]} products per fp32 MAC"),
+                         "vs_fp32_mfma_peak": round(conv_tflops / PEAK_FP32_TFLOPS, 4)},
             "train_tflops_per_gpu": round(3 * FWD_GFLOP_PER_IMG * B / (ms_step * 1e-3) / 1e3, 2),
             "final_loss": loss,
         }

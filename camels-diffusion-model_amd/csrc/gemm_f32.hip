@@ -85,6 +85,15 @@ struct LdDenseAT {  // A(m, k) = a[k*lda + m]  (a is [K][M] row-major, e.g. dY[p
     __device__ __forceinline__ float4 loadT(int k, int m) const {
         return (k < K && m < M) ? ld4(a + (long long)k * lda + m) : f4zero();
     }
+    // split-bf16 path: 8 consecutive k at one m (K % 8 == 0)
+    struct Col { int m; };
+    __device__ __forceinline__ Col col(int m) const { return Col{m}; }
+    __device__ __forceinline__ void load8(const Col& c, int k, float (&o)[8]) const {
+        const bool ok = c.m < M && k < K;
+        const float* p = a + (long long)k * lda + c.m;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = ok ? p[(long long)j * lda] : 0.f;
+    }
 };
 
 // ============================== B loaders, n-contiguous: B(k, n..n+3) ==============================
@@ -111,6 +120,19 @@ struct LdIm2colB {  // conv3x3 wgrad: B(k = pix, n = tap*C + ci) = X[pix shifted
         const int hh = h + c.dy, ww = w + c.dx;
         if ((unsigned)hh >= (unsigned)H || (unsigned)ww >= (unsigned)W) return f4zero();
         return ld4(x + ((long long)(n * H + hh) * W + ww) * ldx + c.ci);
+    }
+    // split-bf16 path: 8 consecutive pixels k..k+7 (one image row, W % 8 == 0) at one column
+    __device__ __forceinline__ void load8(const Col& c, int k, float (&o)[8]) const {
+        const int hw = H * W; const int n = k / hw; const int rem = k - n * hw;
+        const int h = rem / W, w0 = rem - h * W;
+        const int hh = h + c.dy;
+        const bool rowok = c.ok && k < K && (unsigned)hh < (unsigned)H;
+        const float* p = x + ((long long)(n * H + hh) * W + w0 + c.dx) * ldx + c.ci;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int ww = w0 + j + c.dx;
+            o[j] = (rowok && (unsigned)ww < (unsigned)W) ? p[(long long)j * ldx] : 0.f;
+        }
     }
 };
 
@@ -320,6 +342,241 @@ static int effective_splits(int K, int splits, int BK = 16) {
     return ktiles > 0 ? (ktiles + per - 1) / per : 1;
 }
 
+// ============================== split-bf16 main loop (fp32-accurate, bf16 MFMA) ==============================
+// fp32 GEMM on the bf16 matrix cores: every fp32 operand x is split into bf16 terms
+//   x = hi + mid + lo (+ <= 2^-24 |x|),  hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid)
+// and a.b is accumulated (fp32, in the MFMA) from the NT largest cross terms, smallest first:
+//   NT = 6: mm, lh, hl, mh, hm, hh    (dropped: ml, lm, ll <= 2^-24 |ab|  -> fp32-class error)
+//   NT = 3: mh, hm, hh                (~2^-16 relative; bf16x3)
+//   NT = 1: hh                        (plain bf16 operands, fp32 accumulate)
+// v_mfma_f32_32x32x16_bf16 retires 16x the MACs of v_mfma_f32_32x32x2_f32 per cycle, so NT = 6 moves
+// 2.67x the fp32-MFMA rate through the matrix cores.
+// LDS images are [term][row][k] bf16 with a 48-byte row stride: a ds_read_b128 of 16 consecutive rows
+// (or a ds_write_b128 of 16 consecutive rows) touches 16 distinct 16-byte bank groups.
+// Operand stagers (global -> registers -> split -> LDS), one per operand:
+//   StageRowK  rows are k-contiguous fp32 (im2col / dense A): float4 along k, split, ds_write_b64 x terms
+//   StagePre   pre-split bf16 [K/16][3][rows][16] (packed weights, cdm_split_bf16x3): 16-byte copies
+//   StageColK  k-strided fp32 (wgrad: k = pixel, rows = channels): 8 scalar loads along k at one row
+//              (lanes on consecutive rows -> coalesced), split, ds_write_b128 x terms
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+constexpr int XBK = 16;
+constexpr int XSTR = 24;              // bf16 per LDS row (16 used + 8 pad)
+constexpr int XPLANE = GBM * XSTR;    // elements per term plane (GBM == GBN == 128 rows)
+
+template <int NS, int E>
+static __device__ __forceinline__ void split_terms(const float (&x)[E], __bf16 (&h)[E], __bf16 (&m)[E],
+                                                   __bf16 (&l)[E]) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        h[e] = (__bf16)x[e];
+        if constexpr (NS > 1) {
+            const float r = x[e] - (float)h[e];
+            m[e] = (__bf16)r;
+            if constexpr (NS > 2) l[e] = (__bf16)(r - (float)m[e]);
+        }
+    }
+}
+
+template <class LD, int NS>
+struct StageRowK {
+    static constexpr int LDN = GBM * XBK / 4 / GTHREADS;   // 2 float4 per thread
+    LD ld;
+    typename LD::Row row[LDN];
+    float4 r[LDN];
+    __device__ __forceinline__ void init(int tid, int r0) {
+#pragma unroll
+        for (int i = 0; i < LDN; ++i) row[i] = ld.row(r0 + tid / 4 + i * (GTHREADS / 4));
+    }
+    __device__ __forceinline__ void gload(int tid, int kt) {
+#pragma unroll
+        for (int i = 0; i < LDN; ++i) r[i] = ld.load(row[i], kt * XBK + (tid % 4) * 4);
+    }
+    __device__ __forceinline__ void sstore(int tid, __bf16* base) const {
+#pragma unroll
+        for (int i = 0; i < LDN; ++i) {
+            const float x[4] = {r[i].x, r[i].y, r[i].z, r[i].w};
+            __bf16 h[4], m[4], l[4];
+            split_terms<NS>(x, h, m, l);
+            __bf16* d = base + (tid / 4 + i * (GTHREADS / 4)) * XSTR + (tid % 4) * 4;
+            *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
+            if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + XPLANE) = bf16x4{m[0], m[1], m[2], m[3]};
+            if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + 2 * XPLANE) = bf16x4{l[0], l[1], l[2], l[3]};
+        }
+    }
+};
+
+template <int NS>
+struct StagePre {
+    const __bf16* p; int rows;           // [ktiles][3][rows][16]
+    int rr, kh; bool ok;
+    uint4 r[NS];
+    __device__ __forceinline__ void init(int tid, int r0) { rr = r0 + (tid >> 1); kh = (tid & 1) * 8; ok = rr < rows; }
+    __device__ __forceinline__ void gload(int, int kt) {
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+            r[t] = ok ? *reinterpret_cast<const uint4*>(p + (((long long)kt * 3 + t) * rows + rr) * XBK + kh)
+                      : make_uint4(0, 0, 0, 0);
+    }
+    __device__ __forceinline__ void sstore(int tid, __bf16* base) const {
+        __bf16* d = base + (tid >> 1) * XSTR + (tid & 1) * 8;
+#pragma unroll
+        for (int t = 0; t < NS; ++t) *reinterpret_cast<uint4*>(d + t * XPLANE) = r[t];
+    }
+};
+
+template <class LD, int NS>
+struct StageColK {
+    LD ld;
+    typename LD::Col col;
+    float r[8];
+    __device__ __forceinline__ void init(int tid, int r0) { col = ld.col(r0 + (tid & 127)); }
+    __device__ __forceinline__ void gload(int tid, int kt) { ld.load8(col, kt * XBK + (tid >> 7) * 8, r); }
+    __device__ __forceinline__ void sstore(int tid, __bf16* base) const {
+        __bf16 h[8], m[8], l[8];
+        split_terms<NS>(r, h, m, l);
+        __bf16* d = base + (tid & 127) * XSTR + (tid >> 7) * 8;
+        *reinterpret_cast<bf16x8*>(d) = bf16x8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
+        if constexpr (NS > 1)
+            *reinterpret_cast<bf16x8*>(d + XPLANE) = bf16x8{m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7]};
+        if constexpr (NS > 2)
+            *reinterpret_cast<bf16x8*>(d + 2 * XPLANE) = bf16x8{l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7]};
+    }
+};
+
+template <int NT> struct XTerms { static constexpr int NS = NT >= 6 ? 3 : (NT >= 3 ? 2 : 1); };
+
+// SA: operand A stager (rows = M), SB: operand B stager (rows = N); split-K over blockIdx.z.
+template <class SA, class SB, class EP, int NT, bool XCD_REMAP>
+__global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa, SB sb, EP ep, int K, int kt_per_split) {
+    constexpr int NS = XTerms<NT>::NS;
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * NS * XPLANE];
+    __bf16* As = smem;                        // [buf][term][row][XSTR]
+    __bf16* Bs = smem + 2 * NS * XPLANE;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    int bx = blockIdx.x;
+    if constexpr (XCD_REMAP) {
+        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = bx & 7, j = bx >> 3;
+        bx = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int m0 = bx * GBM, n0 = blockIdx.y * GBN;
+    const int ktiles = (K + XBK - 1) / XBK;
+    const int kt0 = blockIdx.z * kt_per_split;
+    const int kt1 = min(ktiles, kt0 + kt_per_split);
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    sa.init(tid, m0);
+    sb.init(tid, n0);
+    if (kt0 < kt1) {
+        sa.gload(tid, kt0); sb.gload(tid, kt0);
+        sa.sstore(tid, As); sb.sstore(tid, Bs);
+    }
+    __syncthreads();
+    int cur = 0;
+    const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31), kh = (lane >> 5) * 8;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) { sa.gload(tid, kt + 1); sb.gload(tid, kt + 1); }
+        const __bf16* a = As + cur * NS * XPLANE;
+        const __bf16* b = Bs + cur * NS * XPLANE;
+        bf16x8 fa[2][NS], fb[2][NS];
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                fa[i][t] = *reinterpret_cast<const bf16x8*>(a + t * XPLANE + (ar + 32 * i) * XSTR + kh);
+                fb[i][t] = *reinterpret_cast<const bf16x8*>(b + t * XPLANE + (br + 32 * i) * XSTR + kh);
+            }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x16 c = acc[i][j];
+                if constexpr (NT >= 6) {
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);   // mm
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);   // lh
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);   // hl
+                }
+                if constexpr (NT >= 3) {
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);   // mh
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);   // hm
+                }
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);  // hh
+            }
+        if (more) {
+            sa.sstore(tid, As + (cur ^ 1) * NS * XPLANE);
+            sb.sstore(tid, Bs + (cur ^ 1) * NS * XPLANE);
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    ep(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
+}
+
+// SA<NS>/SB<NS> are stager templates; splits as launch_gemm (K-tile ranges over blockIdx.z)
+template <template <int> class SAT, template <int> class SBT, class EP, bool XCD_REMAP, class MkA, class MkB>
+static int launch_gemm_x3(MkA mka, MkB mkb, const EP& ep, int M, int N, int K, int splits, int nterm,
+                          hipStream_t s) {
+    const int ktiles = (K + XBK - 1) / XBK;
+    if (splits < 1) splits = 1;
+    if (splits > ktiles) splits = ktiles > 0 ? ktiles : 1;
+    const int per = (ktiles + splits - 1) / splits;
+    splits = ktiles > 0 ? (ktiles + per - 1) / per : 1;
+    dim3 grid((M + GBM - 1) / GBM, (N + GBN - 1) / GBN, splits);
+    switch (nterm) {
+        case 1: hipLaunchKernelGGL((gemm_x3_kernel<SAT<1>, SBT<1>, EP, 1, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
+                                   mka.template make<1>(), mkb.template make<1>(), ep, K, per); break;
+        case 3: hipLaunchKernelGGL((gemm_x3_kernel<SAT<2>, SBT<2>, EP, 3, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
+                                   mka.template make<2>(), mkb.template make<2>(), ep, K, per); break;
+        case 6: hipLaunchKernelGGL((gemm_x3_kernel<SAT<3>, SBT<3>, EP, 6, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
+                                   mka.template make<3>(), mkb.template make<3>(), ep, K, per); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return cdm_status();
+}
+
+template <class LD> struct MkRowK {
+    LD ld;
+    template <int NS> StageRowK<LD, NS> make() const { StageRowK<LD, NS> s; s.ld = ld; return s; }
+};
+template <class LD> struct MkColK {
+    LD ld;
+    template <int NS> StageColK<LD, NS> make() const { StageColK<LD, NS> s; s.ld = ld; return s; }
+};
+struct MkPre {
+    const __bf16* p; int rows;
+    template <int NS> StagePre<NS> make() const { StagePre<NS> s; s.p = p; s.rows = rows; return s; }
+};
+template <class LD> struct RowK { template <int NS> using T = StageRowK<LD, NS>; };
+template <class LD> struct ColK { template <int NS> using T = StageColK<LD, NS>; };
+
+// b [K][N] fp32 (ld ldb)  ->  out [ceil(K/16)][3][N][16] bf16 split terms (k >= K zero-filled)
+__global__ void split_bf16x3_kernel(const float* __restrict__ b, long long ldb, int K, int N, __bf16* __restrict__ out) {
+    const int ktiles = (K + XBK - 1) / XBK;
+    const long long total = (long long)ktiles * N * XBK;
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long long)gridDim.x * blockDim.x) {
+        const int kk = (int)(q % XBK); const long long r = q / XBK;
+        const int n = (int)(r % N); const int kt = (int)(r / N);
+        const int k = kt * XBK + kk;
+        const float x = k < K ? b[(long long)k * ldb + n] : 0.f;
+        const __bf16 h = (__bf16)x;
+        const float r1 = x - (float)h;
+        const __bf16 m = (__bf16)r1;
+        const __bf16 l = (__bf16)(r1 - (float)m);
+        __bf16* o = out + (((long long)kt * 3) * N + n) * XBK + kk;
+        o[0] = h; o[(long long)N * XBK] = m; o[2LL * N * XBK] = l;
+    }
+}
+
 // ============================== slab reduction / permutation ==============================
 // out[m*s_m + (n / csplit)*s_hi + (n % csplit)*s_lo] (+)= sum_z slab[z][m][n]
 __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N, float* out,
@@ -394,6 +651,53 @@ CDM_API int cdm_conv3x3_fwd_variant(int variant, const float* x, int N, int H, i
                 return conv3x3_fwd_bk<16, 16, true>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, st);
         default: return conv3x3_fwd_bk<16, 0, false>(x, N, H, W, Cin, ldx, wpk, bias, y, ldy, Cout, flags, stats, stats_ld, st);
     }
+}
+
+// fp32-accurate conv3x3 forward on the bf16 matrix cores (split terms, see gemm_x3_kernel).
+// wx3 = cdm_split_bf16x3 of the fp32 packed weights (same K order kc as cdm_pack_conv3x3).
+CDM_API int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx3,
+                               const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
+                               int kc, int nterm, void* stream) {
+    if (Cin % 4 || Cout % 4 || (kc != 0 && kc != 16) || (kc == 16 && Cin % 16)) return (int)hipErrorInvalidValue;
+    const int M = N * H * W, K = 9 * Cin;
+    MkPre mb{reinterpret_cast<const __bf16*>(wx3), Cout};
+    EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout};
+    hipStream_t st = S(stream);
+    if (Cin == 128 && Cout == 128 && H == 64 && W == 64 && kc == 16) {
+        using LA = LdIm2colA<128, 16, 64>;
+        return launch_gemm_x3<RowK<LA>::template T, StagePre, EpiStore, true>(MkRowK<LA>{LA{x, H, W, Cin, ldx, M, K}}, mb,
+                                                                             ep, M, Cout, K, 1, nterm, st);
+    }
+    if (kc == 16) {
+        using LA = LdIm2colA<0, 16>;
+        return launch_gemm_x3<RowK<LA>::template T, StagePre, EpiStore, true>(MkRowK<LA>{LA{x, H, W, Cin, ldx, M, K}}, mb,
+                                                                             ep, M, Cout, K, 1, nterm, st);
+    }
+    using LA = LdIm2colA<0, 0>;
+    return launch_gemm_x3<RowK<LA>::template T, StagePre, EpiStore, true>(MkRowK<LA>{LA{x, H, W, Cin, ldx, M, K}}, mb, ep,
+                                                                         M, Cout, K, 1, nterm, st);
+}
+
+// conv3x3 weight gradient on the split-bf16 path (same slab contract as cdm_conv3x3_wgrad); W % 8 == 0
+CDM_API int cdm_conv3x3_wgrad_x3(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,
+                                 int ldx, int splits, float* slab, int nterm, void* stream) {
+    if (Cin % 4 || Cout % 4 || W % 8) return (int)hipErrorInvalidValue;
+    const int M = Cout, NN = 9 * Cin, K = N * H * W;
+    const int sp = effective_splits(K, splits);
+    EpiStore ep{slab, NN, (long long)M * NN, nullptr, 1, 0, nullptr, 0, M, NN};
+    return launch_gemm_x3<ColK<LdDenseAT>::template T, ColK<LdIm2colB>::template T, EpiStore, false>(
+        MkColK<LdDenseAT>{LdDenseAT{dy, lddy, M, K}}, MkColK<LdIm2colB>{LdIm2colB{x, H, W, Cin, ldx, K, NN}}, ep, M, NN,
+        K, sp, nterm, S(stream));
+}
+
+CDM_API int cdm_split_bf16x3(const float* b, long long ldb, int K, int N, void* out, void* stream) {
+    const long long total = (long long)((K + XBK - 1) / XBK) * N * XBK;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(split_bf16x3_kernel, dim3(blocks), dim3(256), 0, S(stream), b, ldb, K, N,
+                       reinterpret_cast<__bf16*>(out));
+    return cdm_status();
 }
 
 CDM_API int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,

@@ -92,16 +92,25 @@ def conv_layers(nf: int, H: int):
     return L
 
 
+# 3x3 conv arithmetic: "fp32" = fp32 MFMA (v_mfma_f32_32x32x2_f32); "x6" = fp32-accurate split-bf16
+# (6 cross terms on v_mfma_f32_32x32x16_bf16, see csrc/gemm_f32.hip); "x3" / "bf16" = reduced-precision
+# variants (bf16x3 / plain bf16 operands, fp32 accumulate) for the mixed-precision configuration.
+CONV_MATH = {"fp32": 0, "x6": 6, "x3": 3, "bf16": 1}
+
 MLPS = ("contextembed1", "timeembed1", "contextembed2", "timeembed2")
 
 
 class UNetEngine:
     """Kernel-level ContextUnet for one (n_feat, n_cfeat, height) on one device."""
 
-    def __init__(self, n_feat: int, n_cfeat: int, height: int, device):
+    def __init__(self, n_feat: int, n_cfeat: int, height: int, device, conv_math: str = "fp32"):
         if n_feat % 8 or height % 16:
             raise ValueError("HIP path needs n_feat % 8 == 0 and height % 16 == 0")
+        if conv_math not in CONV_MATH:
+            raise ValueError(f"conv_math must be one of {sorted(CONV_MATH)}")
         self.nf, self.ncf, self.H = n_feat, n_cfeat, height
+        self.conv_math = conv_math
+        self.nterm = CONV_MATH[conv_math]
         self.device = torch.device(device)
         self.layers = conv_layers(n_feat, height)
         self.L = {l.name: l for l in self.layers}
@@ -129,6 +138,8 @@ class UNetEngine:
                 self.pk[l.name + ".wpk"] = wpk
                 if wdg is not None:
                     self.pk[l.name + ".wdg"] = wdg
+                    self._split(l.name + ".wpk", 9 * l.cin, l.cout, stream)
+                    self._split(l.name + ".wdg", 9 * l.cout, l.cin, stream)
             else:
                 wpk = self._buf(l.name + ".wpk_e", (9 * l.cin, l.cout))
                 bpk = self._buf(l.name + ".bpk_e", (l.cout))
@@ -138,12 +149,17 @@ class UNetEngine:
                                     _p(bpk), None, l.kc, stream)
                 self.pk[l.name + ".wpk_e"] = wpk
                 self.pk[l.name + ".bpk_e"] = bpk
+                if l.cin > 1:
+                    self._split(l.name + ".wpk_e", 9 * l.cin, l.cout, stream)
         # out.0 (GroupNorm follows: never folded)
         wpk = self._buf("out.0.wpk", (9 * 2 * nf, nf))
         wdg = self._buf("out.0.wdg", (9 * nf, 2 * nf))
         lb.cdm_pack_conv3x3(_p(P["out.0.weight"]), _p(P["out.0.bias"]), 2 * nf, nf, None, None, None, None, 0.0,
                             _p(wpk), None, _p(wdg) if train else None, self.kc_out0, stream)
         self.pk["out.0.wpk"], self.pk["out.0.wdg"] = wpk, wdg
+        self._split("out.0.wpk", 9 * 2 * nf, nf, stream)
+        if train:
+            self._split("out.0.wdg", 9 * nf, 2 * nf, stream)
         for name, cin in (("up1.model.0", 4 * nf), ("up2.model.0", 2 * nf)):
             wt = self._buf(name + ".wt", (cin, 4 * nf))
             wtT = self._buf(name + ".wtT", (4 * nf, cin))
@@ -166,12 +182,29 @@ class UNetEngine:
         """Parameters changed behind torch's version counters (fused Adam): drop the cached eval pack."""
         self._pk_key = None
 
-    def _buf(self, name, shape):
+    def _buf(self, name, shape, dtype=torch.float32):
         shape = (shape,) if isinstance(shape, int) else tuple(shape)
         t = self.pk.get(name)
-        if t is None or tuple(t.shape) != tuple(shape):
-            t = torch.empty(*shape, device=self.device, dtype=torch.float32)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.empty(*shape, device=self.device, dtype=dtype)
         return t
+
+    def _split(self, name, K, N, stream):
+        """bf16 hi/mid/lo split of the packed fp32 [K][N] weights pk[name] -> pk[name + "_x"]."""
+        if not self.nterm:
+            return
+        xb = self._buf(name + "_x", (_cdiv(K, 16) * 3 * N * 16,), torch.bfloat16)
+        lib().cdm_split_bf16x3(_p(self.pk[name]), N, K, N, _p(xb), stream)
+        self.pk[name + "_x"] = xb
+
+    def conv3x3(self, key, x_p, B, S, cin, ldx, bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, s):
+        """3x3 conv (fwd or dgrad) with the packed weights pk[key], in this engine's conv arithmetic."""
+        if self.nterm:
+            lib().cdm_conv3x3_fwd_x3(x_p, B, S, S, cin, ldx, _p(self.pk[key + "_x"]), bias_p, y_p, ldy, cout, flags,
+                                     stats_p, stats_ld, kc, self.nterm, s)
+        else:
+            lib().cdm_conv3x3_fwd(x_p, B, S, S, cin, ldx, _p(self.pk[key]), bias_p, y_p, ldy, cout, flags, stats_p,
+                                  stats_ld, kc, s)
 
     # ------------------------------------------------------------------------------------------
     def workspace(self, B: int, train: bool) -> "Workspace":
@@ -242,8 +275,8 @@ class UNetEngine:
         for l in self.layers[14:18]:
             self._conv_bn_fwd(ws, P, l, s, x)
         # ---------------- out ----------------
-        lb.cdm_conv3x3_fwd(ws.catO.p, B, H, H, 2 * nf, 2 * nf, _p(self.pk["out.0.wpk"]), _p(P["out.0.bias"]),
-                           _p(ws.yO), nf, nf, 0, _p(ws.slab), nf, self.kc_out0, s)
+        self.conv3x3("out.0.wpk", ws.catO.p, B, H, 2 * nf, 2 * nf, _p(P["out.0.bias"]), _p(ws.yO), nf, nf, 0,
+                     _p(ws.slab), nf, self.kc_out0, s)
         self._gn_fwd(ws, P, "out.1", Act(ws.yO, nf), B, H, nf, ws.gnO, stats_from_conv=True, stream=s)
         lb.cdm_norm_apply_fwd(APPLY_RELU, _p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]), _p(ws.gnO["shift"]), nf,
                               None, 0, None, 0, None, None, None, 0, _p(ws.zO), nf, s)
@@ -264,8 +297,8 @@ class UNetEngine:
                 lb.cdm_reduce_stats(_p(y), l.cout, B, S * S, l.cout, CHUNK, _p(ws.slab), s)
                 ntiles = B * _cdiv(S * S, CHUNK)
             else:
-                lb.cdm_conv3x3_fwd(src.p, B, S, S, l.cin, src.ld, _p(self.pk[l.name + ".wpk"]), _p(P[l.b]), _p(y),
-                                   l.cout, l.cout, 0, _p(ws.slab), l.cout, l.kc, s)
+                self.conv3x3(l.name + ".wpk", src.p, B, S, l.cin, src.ld, _p(P[l.b]), _p(y), l.cout, l.cout, 0,
+                             _p(ws.slab), l.cout, l.kc, s)
                 ntiles = _cdiv(npix, CHUNK)
             bn = l.bn
             nparts = fold(ws, _p(ws.slab), ntiles, 2, l.cout, s)
@@ -282,8 +315,8 @@ class UNetEngine:
                 lb.cdm_conv3x3_cin1_fwd(_p(x), B, S, S, _p(self.pk[l.name + ".wpk_e"]),
                                         _p(self.pk[l.name + ".bpk_e"]), outp.p, outp.ld, l.cout, 1, s)
             else:
-                lb.cdm_conv3x3_fwd(src.p, B, S, S, l.cin, src.ld, _p(self.pk[l.name + ".wpk_e"]),
-                                   _p(self.pk[l.name + ".bpk_e"]), outp.p, outp.ld, l.cout, EPI_RELU, None, 0, l.kc, s)
+                self.conv3x3(l.name + ".wpk_e", src.p, B, S, l.cin, src.ld, _p(self.pk[l.name + ".bpk_e"]), outp.p,
+                             outp.ld, l.cout, EPI_RELU, None, 0, l.kc, s)
             if dense:
                 return
             scale, shift, relu = self._ones, self._zeros, 0
@@ -350,8 +383,8 @@ class UNetEngine:
                      Act(dyO, nf), G, s)
         # ---------------- out.0 conv (2nf -> nf) ----------------
         self._wgrad3x3(ws, Act(dyO, nf), ws.catO, B, H, 2 * nf, nf, G["out.0.weight"], s)
-        lb.cdm_conv3x3_fwd(_p(dyO), B, H, H, nf, nf, _p(self.pk["out.0.wdg"]), None, ws.dcatO.p, ws.dcatO.ld,
-                           2 * nf, 0, None, 0, self.kc_out0, s)
+        self.conv3x3("out.0.wdg", _p(dyO), B, H, nf, nf, None, ws.dcatO.p, ws.dcatO.ld, 2 * nf, 0, None, 0,
+                     self.kc_out0, s)
         hook("out")
         # ---------------- up2 blocks ----------------
         self._chain_bwd(ws, P, self.layers[14:18], G, s)
@@ -440,13 +473,16 @@ class UNetEngine:
             return
         self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s)
         dgd = ws.dgrad_dst[l.name]
-        lb.cdm_conv3x3_fwd(dy.p, B, S, S, C, dy.ld, _p(self.pk[l.name + ".wdg"]), None, dgd.p, dgd.ld, l.cin,
-                           EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s)
+        self.conv3x3(l.name + ".wdg", dy.p, B, S, C, dy.ld, None, dgd.p, dgd.ld, l.cin,
+                     EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s)
 
     def _wgrad3x3(self, ws, dy: Act, x: Act, B, S, cin, cout, gW, s):
         lb = lib()
         sp = wgrad_splits(B * S * S, cout, 9 * cin)
-        lb.cdm_conv3x3_wgrad(dy.p, dy.ld, cout, x.p, B, S, S, cin, x.ld, sp, _p(ws.slab), s)
+        if self.nterm:
+            lb.cdm_conv3x3_wgrad_x3(dy.p, dy.ld, cout, x.p, B, S, S, cin, x.ld, sp, _p(ws.slab), self.nterm, s)
+        else:
+            lb.cdm_conv3x3_wgrad(dy.p, dy.ld, cout, x.p, B, S, S, cin, x.ld, sp, _p(ws.slab), s)
         # slab[z][co][tap*cin+ci] -> OIHW [co][ci][tap]
         lb.cdm_slab_reduce(_p(ws.slab), sp, cout, 9 * cin, _p(gW), 9 * cin, 1, 9, cin, 0, 1.0, s)
 

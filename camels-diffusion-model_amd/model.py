@@ -14,12 +14,13 @@ used by the captured train/sample loops).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
 import torch.nn as nn
 
-from .engine import UNetEngine
+from .engine import CONV_MATH, UNetEngine
 
 # ------------------------------------------------------------------------------------------------
 # building blocks (constructor-compatible with code/diffusion_utilities.py)
@@ -84,13 +85,19 @@ class EmbedFC(_Holder):
 _ENGINES: Dict[tuple, UNetEngine] = {}
 
 
-def get_engine(n_feat, n_cfeat, height, device) -> UNetEngine:
+def get_engine(n_feat, n_cfeat, height, device, conv_math: str = "fp32") -> UNetEngine:
     dev = torch.device(device)
-    key = (n_feat, n_cfeat, height, dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+    key = (n_feat, n_cfeat, height, dev.type, dev.index if dev.index is not None else torch.cuda.current_device(),
+           conv_math)
     eng = _ENGINES.get(key)
     if eng is None:
-        eng = _ENGINES[key] = UNetEngine(n_feat, n_cfeat, height, dev)
+        eng = _ENGINES[key] = UNetEngine(n_feat, n_cfeat, height, dev, conv_math)
     return eng
+
+
+def default_conv_math() -> str:
+    """3x3 conv arithmetic used when ContextUnet(conv_math=None): $CDM_CONV_MATH or "fp32"."""
+    return os.environ.get("CDM_CONV_MATH", "fp32")
 
 
 def _stream() -> int:
@@ -126,8 +133,12 @@ class _UNetFunction(torch.autograd.Function):
 class ContextUnet(nn.Module):
     """Drop-in for ContextUnet.py:5-60 (same constructor, attributes, state_dict and forward)."""
 
-    def __init__(self, in_channels, n_feat=128, n_cfeat=10, height=64, shortcut_source: str = "cpu"):
+    def __init__(self, in_channels, n_feat=128, n_cfeat=10, height=64, shortcut_source: str = "cpu",
+                 conv_math: Optional[str] = None):
         super().__init__()
+        self.conv_math = conv_math or default_conv_math()
+        if self.conv_math not in CONV_MATH:
+            raise ValueError(f"conv_math must be one of {sorted(CONV_MATH)}")
         self.in_channels, self.n_feat, self.n_cfeat, self.h = in_channels, n_feat, n_cfeat, height
         # construction order == reference order, so seeded default init reproduces its weights
         self.init_conv = ResidualConvBlock(in_channels, n_feat, is_res=True)
@@ -165,7 +176,7 @@ class ContextUnet(nn.Module):
                 continue
             if v.dtype != torch.float32 or not v.is_contiguous():
                 raise RuntimeError(f"{k}: expected contiguous fp32 (got {v.dtype})")
-        return get_engine(self.n_feat, self.n_cfeat, self.h, dev), P
+        return get_engine(self.n_feat, self.n_cfeat, self.h, dev, self.conv_math), P
 
     def _invalidate_eval_pack(self):
         self._eval_key = None

@@ -35,6 +35,17 @@ int cdm_conv3x3_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const
 int cdm_conv3x3_fwd_variant(int variant, const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,
                             const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
                             void* stream);
+/* conv3x3 forward, fp32-accurate on the bf16 matrix cores: operands split into nterm-term bf16 sums
+ * (nterm 6 = fp32-class, 3 = bf16x3, 1 = bf16); wx3 from cdm_split_bf16x3 of the packed weights.
+ * Same semantics as cdm_conv3x3_fwd (nn.Conv2d(.,.,3,1,1) diffusion_utilities.py:27,34). */
+int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx3, const float* bias,
+                       float* y, int ldy, int Cout, int flags, float* stats, int stats_ld, int kc, int nterm,
+                       void* stream);
+/* conv3x3 weight gradient on the split-bf16 path: same slab contract as cdm_conv3x3_wgrad; W % 8 == 0 */
+int cdm_conv3x3_wgrad_x3(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,
+                         int splits, float* slab, int nterm, void* stream);
+/* fp32 [K][N] (ld ldb) -> [ceil(K/16)][3][N][16] bf16 split terms hi/mid/lo */
+int cdm_split_bf16x3(const float* b, long long ldb, int K, int N, void* out, void* stream);
 /* nn.ConvTranspose2d(Cin,Cout,2,2) forward (diffusion_utilities.py:86); H,W = input grid. */
 int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk, const float* bias,
                      float* y, int ldy, int Cout, void* stream);

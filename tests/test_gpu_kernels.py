@@ -161,3 +161,61 @@ def test_gemm_and_tn(L, M, K, N, splits):
     L.cdm_slab_reduce(slab.data_ptr(), sp, Mt, N, out.data_ptr(), N, 0, 1, N, 0, 1.0, _s())
     torch.cuda.synchronize()
     _close(out, reft, 5e-5)
+
+
+@pytest.mark.parametrize("nterm,tol", [(6, 2e-5), (3, 2e-4), (1, 2e-2)])
+@pytest.mark.parametrize("N,H,Cin,Cout,kc", [(2, 16, 32, 64, 16), (1, 64, 128, 128, 16), (3, 8, 8, 16, 0),
+                                              (2, 32, 256, 128, 16), (1, 8, 12, 20, 0)])
+def test_conv3x3_split_bf16(L, N, H, Cin, Cout, kc, nterm, tol):
+    """cdm_conv3x3_fwd_x3 (split-bf16 MFMA) fwd + dgrad + stats against torch fp32 conv."""
+    torch.manual_seed(4)
+    x = torch.randn(N, Cin, H, H); W = torch.randn(Cout, Cin, 3, 3) * 0.1; b = torch.randn(Cout)
+    gy = torch.randn(N, Cout, H, H)
+    xg, Wg = x.clone().requires_grad_(), W.clone().requires_grad_()
+    ref = F.conv2d(xg, Wg, b, padding=1)
+    ref.backward(gy)
+    Wc, bc = W.cuda(), b.cuda()
+    wpk, wdg = _pack3x3(L, Wc, bc, kc)
+    split = lambda w, K, NN: _split(L, w, K, NN)
+    wx, wdx = split(wpk, 9 * Cin, Cout), split(wdg, 9 * Cout, Cin)
+    y = torch.empty(N * H * H, Cout, device="cuda")
+    stats = torch.zeros((N * H * H + 127) // 128, 2, Cout, device="cuda")
+    xn0, gyn0 = _nhwc(x), _nhwc(gy)
+    L.cdm_conv3x3_fwd_x3(xn0.data_ptr(), N, H, H, Cin, Cin, wx.data_ptr(), bc.data_ptr(), y.data_ptr(), Cout,
+                         Cout, 0, stats.data_ptr(), Cout, kc, nterm, _s())
+    dx = torch.empty(N * H * H, Cin, device="cuda")
+    L.cdm_conv3x3_fwd_x3(gyn0.data_ptr(), N, H, H, Cout, Cout, wdx.data_ptr(), None, dx.data_ptr(), Cin, Cin, 0,
+                         None, 0, kc, nterm, _s())
+    torch.cuda.synchronize()
+    _close(_nchw(y, N, H, H, Cout), ref.detach(), tol)
+    _close(_nchw(dx, N, H, H, Cin), xg.grad, tol)
+    ysum = ref.detach().permute(0, 2, 3, 1).reshape(-1, Cout)
+    _close(stats[:, 0].sum(0), ysum.sum(0), max(tol, 1e-4))
+    gyn, xn = _nhwc(gy), _nhwc(x)   # keep both alive: the launch is asynchronous
+    for splits in (1, 7):   # weight gradient, split-K slabs
+        sp = L.raw("cdm_gemm_splits")(N * H * H, splits)
+        slab = torch.empty(sp, Cout, 9 * Cin, device="cuda")
+        L.cdm_conv3x3_wgrad_x3(gyn.data_ptr(), Cout, Cout, xn.data_ptr(), N, H, H, Cin, Cin, sp, slab.data_ptr(),
+                               nterm, _s())
+        dW = torch.empty(Cout, Cin, 3, 3, device="cuda")
+        L.cdm_slab_reduce(slab.data_ptr(), sp, Cout, 9 * Cin, dW.data_ptr(), 9 * Cin, 1, 9, Cin, 0, 1.0, _s())
+        torch.cuda.synchronize()
+        _close(dW, Wg.grad, max(tol, 5e-5))
+
+
+def _split(L, w, K, NN):
+    out = torch.empty(((K + 15) // 16) * 3 * NN * 16, dtype=torch.bfloat16, device="cuda")
+    L.cdm_split_bf16x3(w.data_ptr(), NN, K, NN, out.data_ptr(), _s())
+    return out
+
+
+def test_split_bf16x3_terms_sum_to_fp32(L):
+    """hi + mid + lo reproduces every fp32 weight to <= 2^-24 relative; layout [K/16][3][N][16]."""
+    torch.manual_seed(5)
+    K, NN = 40, 12
+    w = (torch.randn(K, NN) * torch.logspace(-3, 3, K)[:, None]).cuda()
+    xs = _split(L, w, K, NN).float().reshape(-1, 3, NN, 16)          # [kt][term][n][kk]
+    rec = xs.double().sum(1).permute(0, 2, 1).reshape(-1, NN)[:K]   # [k][n]
+    err = ((rec - w.double()).abs() / w.double().abs()).max().item()
+    assert err <= 2.0 ** -24, err
+    assert xs.reshape(-1, 3, NN, 16).permute(0, 3, 1, 2).reshape(-1, 3, NN)[K:].abs().max().item() == 0.0

@@ -44,8 +44,9 @@ def test_calculate_likelihood_matches_reference():
     import cdm_amd
     lfx = np.load(os.path.join(GOLD, "likelihood_nf8.npz"))
     T = int(lfx["T_lik"])
+    m = _model()                    # construct first: default init consumes the CPU RNG
     torch.manual_seed(600)
-    nll = cdm_amd.calculate_likelihood(_model(), _batches(lfx), T, "cuda", noise_source="host")
+    nll = cdm_amd.calculate_likelihood(m, _batches(lfx), T, "cuda", noise_source="host")
     _close(nll, float(lfx["nll_elbo_script"]), 1e-4)
 
 
@@ -53,8 +54,8 @@ def test_calculate_elbo_and_bpd_dataset_matches_reference():
     import cdm_amd
     lfx = np.load(os.path.join(GOLD, "likelihood_nf8.npz"))
     T = int(lfx["T_elbo"])
-    torch.manual_seed(601)
     m = _model()
+    torch.manual_seed(601)
     elbo, bpd = cdm_amd.calculate_elbo_and_bpd(m, _batches(lfx), T, "cuda", noise_source="host")
     _close(elbo, float(lfx["paper_elbo"]), 1e-4)
     _close(bpd, float(lfx["paper_bpd"]), 1e-4)

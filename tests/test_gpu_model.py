@@ -1,5 +1,8 @@
 """Whole-model parity of the HIP ContextUnet against the CPU oracle / reference golden vectors.
 
+Every test runs with both 3x3-conv arithmetics: "fp32" (fp32 MFMA) and "x6" (fp32-accurate split-bf16
+MFMA, 6 cross terms) — same tolerances, so x6 is held to the fp32 bar.
+
 Tolerances (fp32 everywhere; only summation order differs):
   forward eps            max|d| <= 1e-4 * max|ref|
   parameter gradients    per tensor  max|d| <= 2e-3 * max|ref| + 1e-4 * max over all grads of max|ref|
@@ -24,10 +27,13 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-def _model(nf, ncf=6, sd=None, seed=0):
+MATH = pytest.mark.parametrize("math", ["fp32", "x6"])
+
+
+def _model(nf, ncf=6, sd=None, seed=0, math="fp32"):
     from cdm_amd import ContextUnet
     torch.manual_seed(seed)
-    m = ContextUnet(1, nf, ncf, 64)
+    m = ContextUnet(1, nf, ncf, 64, conv_math=math)
     if sd is not None:
         m.load_state_dict({k: torch.as_tensor(v) for k, v in sd.items()})
     return m.cuda()
@@ -46,10 +52,11 @@ def _rel(got, ref):
     return (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
 
 
+@MATH
 @pytest.mark.parametrize("nf", [8, 16])
-def test_eval_forward_matches_reference(nf):
+def test_eval_forward_matches_reference(nf, math):
     fx = _fx(f"model_nf{nf}.npz")
-    m = _model(nf, sd=_sd(fx)).eval()
+    m = _model(nf, sd=_sd(fx), math=math).eval()
     x, t, c = (torch.from_numpy(fx[k]).cuda() for k in ("x", "t", "c"))
     with torch.no_grad():
         torch.manual_seed(11)                 # the reference drew its shortcut from this seed
@@ -61,10 +68,11 @@ def test_eval_forward_matches_reference(nf):
         assert _rel(eps, torch.from_numpy(fx["eval_uncond_eps"])) < 1e-4
 
 
-def test_train_step_grads_match_reference():
+@MATH
+def test_train_step_grads_match_reference(math):
     fx = _fx("model_nf8.npz")
     nf, T = 8, int(fx["train_T"])
-    m = _model(nf, sd=_sd(fx)).train()
+    m = _model(nf, sd=_sd(fx), math=math).train()
     c = torch.from_numpy(fx["c"]).cuda()
     xp = torch.from_numpy(fx["train0_xpert"]).cuda()
     noise = torch.from_numpy(fx["train0_noise"]).cuda()
@@ -106,9 +114,10 @@ def test_running_stats_update():
             assert err <= 1e-5 * ref.abs().max().item() + 1e-6, k
 
 
+@MATH
 @pytest.mark.parametrize("nf,B", [(64, 3), (128, 2)])
-def test_forward_random_weights_vs_oracle(nf, B):
-    m = _model(nf, seed=3)
+def test_forward_random_weights_vs_oracle(nf, B, math):
+    m = _model(nf, seed=3, math=math)
     g = torch.Generator().manual_seed(9)
     x = torch.rand(B, 1, 64, 64, generator=g); t = torch.rand(B, generator=g); c = torch.rand(B, 6, generator=g)
     sd = R.clone_sd(m.state_dict())
@@ -133,7 +142,8 @@ def _oracle_grads(sd, x, c, noise, tt, T, ab, nf, dtype, seed):
     return pred, grads
 
 
-def test_train_grads_random_weights_nf64():
+@MATH
+def test_train_grads_random_weights_nf64(math):
     """HIP grads vs an fp64 oracle, at the accuracy the reference's own fp32 CPU path has.
 
     Rationale: with ReLU + MaxPool, last-bit differences flip a handful of kink decisions (|z| ~ 1e-6)
@@ -144,7 +154,7 @@ def test_train_grads_random_weights_nf64():
     noise only): |g| <= 1e-4 * max grad.  The strict check lives in test_train_step_grads_match_reference.
     """
     nf, B, T = 64, 2, 1500
-    m = _model(nf, seed=4).train()
+    m = _model(nf, seed=4, math=math).train()
     sd = R.clone_sd(m.state_dict())
     g = torch.Generator().manual_seed(10)
     x = torch.rand(B, 1, 64, 64, generator=g); noise = torch.randn(B, 1, 64, 64, generator=g)

@@ -8,7 +8,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(n=10, B=256, H=64, C=128, variant=-1):
+def main(n=10, B=256, H=64, C=128, variant=-1, nterm=0):
     import cdm_amd
     L = cdm_amd.lib()
     s = torch.cuda.current_stream().cuda_stream
@@ -21,8 +21,13 @@ def main(n=10, B=256, H=64, C=128, variant=-1):
                        16 if variant in (-1, 3, 4) else 0, s)
     y = torch.empty(B * H * H, C, device="cuda")
     st = torch.empty((B * H * H + 127) // 128, 2, C, device="cuda")
+    wx = torch.empty(9 * C // 16 * 3 * C * 16, dtype=torch.bfloat16, device="cuda")
+    L.cdm_split_bf16x3(wpk.data_ptr(), C, 9 * C, C, wx.data_ptr(), s)
     for _ in range(n):
-        if variant < 0:    # the shipped path (engine / bench)
+        if nterm:          # split-bf16 path (conv_math x6 / x3 / bf16)
+            L.cdm_conv3x3_fwd_x3(x.data_ptr(), B, H, H, C, C, wx.data_ptr(), b.data_ptr(), y.data_ptr(), C, C, 0,
+                                 st.data_ptr(), C, 16, nterm, s)
+        elif variant < 0:    # the fp32 path
             L.cdm_conv3x3_fwd(x.data_ptr(), B, H, H, C, C, wpk.data_ptr(), b.data_ptr(), y.data_ptr(), C, C, 0,
                               st.data_ptr(), C, 16, s)
         else:
@@ -33,4 +38,7 @@ def main(n=10, B=256, H=64, C=128, variant=-1):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10, variant=int(sys.argv[2]) if len(sys.argv) > 2 else -1)
+    # argv: [n] [variant (fp32 path) | x6 | x3 | x1]
+    arg = sys.argv[2] if len(sys.argv) > 2 else "-1"
+    nt = int(arg[1:]) if arg.startswith("x") else 0
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10, variant=-1 if nt else int(arg), nterm=nt)
