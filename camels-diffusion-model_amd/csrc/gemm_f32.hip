@@ -164,7 +164,8 @@ struct LdConvT2x2GatherB {  // convT 2x2 wgrad: B(k = input pix (n,h,w), n = ij*
 
 enum { EPI_RELU = 1, EPI_ACCUM = 2 };
 
-struct EpiStore {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-tile column stats
+template <int WM = 2>   // WM = waves along M (2: 128-row block, 4: 256-row block); stats per 128-row tile
+struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-tile column stats
     float* y; long long ldy; long long zstride; const float* bias; int bias_mod; int flags;
     float* stats; int stats_ld;  // stats[tile][0|1][stats_ld]: sum / sum of squares of the stored value
     int M, N;
@@ -197,16 +198,18 @@ struct EpiStore {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-t
             }
         }
         __syncthreads();
-        if (tid < GBN) {
-            const int n = blockIdx.y * GBN + tid;
+        if (tid < GBN * (WM / 2)) {   // tile t of the block's WM/2 128-row tiles sums waves 2t and 2t+1
+            const int t = tid / GBN, c = tid - t * GBN;
+            const int n = blockIdx.y * GBN + c;
             if (n < N) {
-                float* st = stats + (long long)(mw / GBM) * 2 * stats_ld;
-                st[n] = scratch[0 * GBN + tid] + scratch[2 * GBN + tid];
-                st[stats_ld + n] = scratch[1 * GBN + tid] + scratch[3 * GBN + tid];
+                float* st = stats + (long long)((mw - wm * 64) / GBM + t) * 2 * stats_ld;
+                st[n] = scratch[(4 * t + 0) * GBN + c] + scratch[(4 * t + 2) * GBN + c];
+                st[stats_ld + n] = scratch[(4 * t + 1) * GBN + c] + scratch[(4 * t + 3) * GBN + c];
             }
         }
     }
 };
+using EpiStore = EpiStoreW<2>;
 
 struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n, 2h+i, 2w+j, co] = acc + b[co]
     float* y; long long ldy; const float* bias; int H, W, Co, M, N;
@@ -351,8 +354,11 @@ static int effective_splits(int K, int splits, int BK = 16) {
 //   NT = 1: hh                        (plain bf16 operands, fp32 accumulate)
 // v_mfma_f32_32x32x16_bf16 retires 16x the MACs of v_mfma_f32_32x32x2_f32 per cycle, so NT = 6 moves
 // 2.67x the fp32-MFMA rate through the matrix cores.
-// LDS images are [term][row][k] bf16 with a 48-byte row stride: a ds_read_b128 of 16 consecutive rows
-// (or a ds_write_b128 of 16 consecutive rows) touches 16 distinct 16-byte bank groups.
+// LDS images are [term][row][16 k] bf16, 32 bytes per row, no padding; the two 16-byte k-halves of a
+// row are XOR-swizzled by row bit 3 (xoff below).  With the gfx950 LDS lane groups this makes every
+// access conflict-free: fragment ds_read_b128 (4 x 16 lanes, 256-byte banks), the A ds_write_b64
+// (4 x 16 lanes = 4 rows x 32 B, 128-byte banks) and the B / k-strided ds_write_b128 (8 x 8 lanes = 4 rows
+// x 2 halves).  (PMC on the previous 48-byte padded stride: 33 % of LDS cycles were bank conflicts.)
 // Operand stagers (global -> registers -> split -> LDS), one per operand:
 //   StageRowK  rows are k-contiguous fp32 (im2col / dense A): float4 along k, split, ds_write_b64 x terms
 //   StagePre   pre-split bf16 [K/16][3][rows][16] (packed weights, cdm_split_bf16x3): 16-byte copies
@@ -361,8 +367,12 @@ static int effective_splits(int K, int splits, int BK = 16) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int XBK = 16;
-constexpr int XSTR = 24;              // bf16 per LDS row (16 used + 8 pad)
-constexpr int XPLANE = GBM * XSTR;    // elements per term plane (GBM == GBN == 128 rows)
+constexpr int XPLANE = GBM * XBK;     // elements per term plane (GBM == GBN == 128 rows x 16 k)
+
+// element offset of (row, k) in a term plane: 16 bf16 per row, k-halves swapped on odd row-octets
+static __device__ __forceinline__ int xoff(int row, int k) {
+    return row * XBK + ((((k >> 3) ^ (row >> 3)) & 1) << 3) + (k & 7);
+}
 
 template <int NS, int E>
 static __device__ __forceinline__ void split_terms(const float (&x)[E], __bf16 (&h)[E], __bf16 (&m)[E],
@@ -398,7 +408,7 @@ struct StageRowK {
             const float x[4] = {r[i].x, r[i].y, r[i].z, r[i].w};
             __bf16 h[4], m[4], l[4];
             split_terms<NS>(x, h, m, l);
-            __bf16* d = base + (tid / 4 + i * (GTHREADS / 4)) * XSTR + (tid % 4) * 4;
+            __bf16* d = base + xoff(tid / 4 + i * (GTHREADS / 4), (tid % 4) * 4);
             *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
             if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + XPLANE) = bf16x4{m[0], m[1], m[2], m[3]};
             if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + 2 * XPLANE) = bf16x4{l[0], l[1], l[2], l[3]};
@@ -419,7 +429,7 @@ struct StagePre {
                       : make_uint4(0, 0, 0, 0);
     }
     __device__ __forceinline__ void sstore(int tid, __bf16* base) const {
-        __bf16* d = base + (tid >> 1) * XSTR + (tid & 1) * 8;
+        __bf16* d = base + xoff(tid >> 1, (tid & 1) * 8);
 #pragma unroll
         for (int t = 0; t < NS; ++t) *reinterpret_cast<uint4*>(d + t * XPLANE) = r[t];
     }
@@ -430,12 +440,13 @@ struct StageColK {
     LD ld;
     typename LD::Col col;
     float r[8];
-    __device__ __forceinline__ void init(int tid, int r0) { col = ld.col(r0 + (tid & 127)); }
-    __device__ __forceinline__ void gload(int tid, int kt) { ld.load8(col, kt * XBK + (tid >> 7) * 8, r); }
+    // thread -> (row tid>>1, k-half tid&1): an 8-lane store group covers 4 rows x 2 halves (conflict-free)
+    __device__ __forceinline__ void init(int tid, int r0) { col = ld.col(r0 + (tid >> 1)); }
+    __device__ __forceinline__ void gload(int tid, int kt) { ld.load8(col, kt * XBK + (tid & 1) * 8, r); }
     __device__ __forceinline__ void sstore(int tid, __bf16* base) const {
         __bf16 h[8], m[8], l[8];
         split_terms<NS>(r, h, m, l);
-        __bf16* d = base + (tid & 127) * XSTR + (tid >> 7) * 8;
+        __bf16* d = base + xoff(tid >> 1, (tid & 1) * 8);
         *reinterpret_cast<bf16x8*>(d) = bf16x8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
         if constexpr (NS > 1)
             *reinterpret_cast<bf16x8*>(d + XPLANE) = bf16x8{m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7]};
@@ -451,7 +462,7 @@ template <class SA, class SB, class EP, int NT, bool XCD_REMAP>
 __global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa, SB sb, EP ep, int K, int kt_per_split) {
     constexpr int NS = XTerms<NT>::NS;
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * NS * XPLANE];
-    __bf16* As = smem;                        // [buf][term][row][XSTR]
+    __bf16* As = smem;                        // [buf][term][row][16 k] (xoff swizzle)
     __bf16* Bs = smem + 2 * NS * XPLANE;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -483,6 +494,9 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa, SB sb, EP e
     __syncthreads();
     int cur = 0;
     const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31), kh = (lane >> 5) * 8;
+    int aoff[2], boff[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) { aoff[i] = xoff(ar + 32 * i, kh); boff[i] = xoff(br + 32 * i, kh); }
     for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = kt + 1 < kt1;
         if (more) { sa.gload(tid, kt + 1); sb.gload(tid, kt + 1); }
@@ -493,8 +507,8 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa, SB sb, EP e
         for (int t = 0; t < NS; ++t)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                fa[i][t] = *reinterpret_cast<const bf16x8*>(a + t * XPLANE + (ar + 32 * i) * XSTR + kh);
-                fb[i][t] = *reinterpret_cast<const bf16x8*>(b + t * XPLANE + (br + 32 * i) * XSTR + kh);
+                fa[i][t] = *reinterpret_cast<const bf16x8*>(a + t * XPLANE + aoff[i]);
+                fb[i][t] = *reinterpret_cast<const bf16x8*>(b + t * XPLANE + boff[i]);
             }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -558,6 +572,190 @@ struct MkPre {
 };
 template <class LD> struct RowK { template <int NS> using T = StageRowK<LD, NS>; };
 template <class LD> struct ColK { template <int NS> using T = StageColK<LD, NS>; };
+
+// ============================== LDS-halo conv3x3 on the split-bf16 matrix cores ==============================
+// conv3x3 (stride 1, pad 1) forward / dgrad for Cin % 16 == 0 (channel-chunk-major K, kc = 16) and image
+// width WT in {32, 64}.  A block owns 256 consecutive output pixels (= 256/WT whole image rows) x 128
+// output channels, 8 waves as 4 (M) x 2 (N), each wave 64x64.  Per 16-channel chunk the block stages its
+// input rows plus the 1-pixel halo ((256/WT + 2) x (WT + 2) pixels x 16 ch) ONCE into LDS, split into
+// bf16 terms, and the 9 taps of that chunk read their A fragments straight out of the halo tile at
+// shifted addresses: no im2col re-reads (the generic path re-reads every input element 9x through
+// L1/L2).  B (pre-split weights) streams one kernel row (3 taps, 36 KiB) per barrier, double-buffered,
+// so each barrier interval holds 72 MFMAs per wave and the fragment reads of tap t+1 overlap the MFMAs
+// of tap t; 256-row blocks halve the per-pixel weight re-reads of the 128-row kernel.
+// LDS (x6, WT 64): halo 2 x 3 x 396 px x 32 B + B 2 x 3 taps x 3 terms x 4 KiB = 146 KiB (1 block / CU).
+constexpr int HBM_ = 256;          // output pixels per block
+constexpr int HTHREADS = 512;
+
+template <int NT, int WT, class EP, bool XCD_REMAP>
+__global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const float* __restrict__ x, int H, int Cin,
+                                                                      int ldx, const __bf16* __restrict__ wx3,
+                                                                      int Cout, EP ep) {
+    constexpr int NS = XTerms<NT>::NS;
+    constexpr int ROWS = HBM_ / WT, HR = ROWS + 2, HC = WT + 2, HPX = HR * HC;
+    constexpr int HPLANE = HPX * XBK;                 // bf16 per halo term plane
+    constexpr int HQ = (HPX * 4 + HTHREADS - 1) / HTHREADS;   // float4 halo pieces per thread
+    constexpr int BPL = 3 * NS;                       // B planes per group (3 taps x NS terms)
+    constexpr int BQ = (BPL * 256 + HTHREADS - 1) / HTHREADS;  // 16-byte B pieces per thread
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * NS * HPLANE + 2 * BPL * XPLANE];
+    __bf16* Hs = smem;                                // [buf][term][halo pixel][16 ch] (xoff swizzle)
+    __bf16* Bs = smem + 2 * NS * HPLANE;              // [buf][tap dx][term][col][16 k] (xoff swizzle)
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    int bx = blockIdx.x;
+    if constexpr (XCD_REMAP) {
+        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = bx & 7, j = bx >> 3;
+        bx = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int m0 = bx * HBM_, n0 = blockIdx.y * GBN;
+    const int hw = H * WT, img = m0 / hw, h0 = (m0 - img * hw) / WT;
+    const int nchunks = Cin / 16, ngroups = nchunks * 3;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // ---- halo staging: piece q = (halo pixel q>>2, channels 4(q&3)..+3) ----
+    float4 hreg[HQ];
+    auto gload_halo = [&](int cc) {
+#pragma unroll
+        for (int j = 0; j < HQ; ++j) {
+            const int q = tid + j * HTHREADS;
+            const int hp = q >> 2, c4 = q & 3;
+            const int hr = hp / HC, hc = hp - hr * HC;
+            const int ih = h0 - 1 + hr, iw = hc - 1;
+            hreg[j] = (q < HPX * 4 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)WT)
+                          ? ld4(x + ((long long)(img * H + ih) * WT + iw) * ldx + cc * 16 + c4 * 4)
+                          : f4zero();
+        }
+    };
+    auto store_halo = [&](__bf16* base) {
+#pragma unroll
+        for (int j = 0; j < HQ; ++j) {
+            const int q = tid + j * HTHREADS;
+            if (q < HPX * 4) {
+                const float xv[4] = {hreg[j].x, hreg[j].y, hreg[j].z, hreg[j].w};
+                __bf16 h[4], m[4], l[4];
+                split_terms<NS>(xv, h, m, l);
+                __bf16* d = base + xoff(q >> 2, (q & 3) * 4);
+                *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
+                if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + HPLANE) = bf16x4{m[0], m[1], m[2], m[3]};
+                if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + 2 * HPLANE) = bf16x4{l[0], l[1], l[2], l[3]};
+            }
+        }
+    };
+    // ---- B staging: piece q = (plane q>>8 = dx*NS + t, col (q&255)>>1, k-half q&1) of group g ----
+    uint4 breg[BQ];
+    auto gload_b = [&](int g) {
+#pragma unroll
+        for (int j = 0; j < BQ; ++j) {
+            const int q = tid + j * HTHREADS;
+            const int pl = q >> 8, dx = pl / NS, t = pl - dx * NS, rr = (q & 255) >> 1, half = q & 1;
+            const int n = n0 + rr;
+            breg[j] = (q < BPL * 256 && n < Cout)
+                          ? *reinterpret_cast<const uint4*>(wx3 + (((long long)(g * 3 + dx) * 3 + t) * Cout + n) * XBK +
+                                                            half * 8)
+                          : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto store_b = [&](__bf16* base) {
+#pragma unroll
+        for (int j = 0; j < BQ; ++j) {
+            const int q = tid + j * HTHREADS;
+            if (q < BPL * 256)
+                *reinterpret_cast<uint4*>(base + (q >> 8) * XPLANE + xoff((q & 255) >> 1, (q & 1) * 8)) = breg[j];
+        }
+    };
+
+    // per-lane halo pixel of each A fragment row (tap (0,0) origin)
+    const int kh = (lane >> 5) * 8;
+    int hp0[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int p = wm * 64 + 32 * i + (lane & 31);
+        const int r = p / WT, c = p - r * WT;
+        hp0[i] = r * HC + c;
+    }
+    int boff[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) boff[j] = xoff(wn * 64 + 32 * j + (lane & 31), kh);
+
+    gload_halo(0);
+    gload_b(0);
+    store_halo(Hs);
+    store_b(Bs);
+    __syncthreads();
+    int hb = 0, bb = 0;
+    for (int cc = 0; cc < nchunks; ++cc) {
+        const bool morec = cc + 1 < nchunks;
+        if (morec) gload_halo(cc + 1);
+#pragma unroll 1
+        for (int dy = 0; dy < 3; ++dy) {
+            const int g = cc * 3 + dy;
+            const bool moreg = g + 1 < ngroups;
+            if (moreg) gload_b(g + 1);
+            const __bf16* a = Hs + hb * NS * HPLANE;
+            const __bf16* b = Bs + bb * BPL * XPLANE;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                bf16x8 fa[2][NS], fb[2][NS];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int ao = xoff(hp0[i] + dy * HC + dx, kh);
+#pragma unroll
+                    for (int t = 0; t < NS; ++t) {
+                        fa[i][t] = *reinterpret_cast<const bf16x8*>(a + t * HPLANE + ao);
+                        fb[i][t] = *reinterpret_cast<const bf16x8*>(b + (dx * NS + t) * XPLANE + boff[i]);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        f32x16 c = acc[i][j];
+                        if constexpr (NT >= 6) {
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+                        }
+                        if constexpr (NT >= 3) {
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+                        }
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+                    }
+            }
+            if (moreg) store_b(Bs + (bb ^ 1) * BPL * XPLANE);
+            if (dy == 0 && morec) store_halo(Hs + (hb ^ 1) * NS * HPLANE);   // buffer idle since chunk cc-1
+            __syncthreads();
+            bb ^= 1;
+        }
+        hb ^= 1;
+    }
+    ep(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
+}
+
+template <int WT>
+static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
+                            const EpiStoreW<4>& ep, int nterm, hipStream_t s) {
+    const int M = N * H * WT;
+    dim3 grid(M / HBM_, (Cout + GBN - 1) / GBN, 1);
+    switch (nterm) {
+        case 1: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true>), grid, dim3(HTHREADS), 0, s, x, H,
+                                   Cin, ldx, wx3, Cout, ep); break;
+        case 3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<3, WT, EpiStoreW<4>, true>), grid, dim3(HTHREADS), 0, s, x, H,
+                                   Cin, ldx, wx3, Cout, ep); break;
+        case 6: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<6, WT, EpiStoreW<4>, true>), grid, dim3(HTHREADS), 0, s, x, H,
+                                   Cin, ldx, wx3, Cout, ep); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return cdm_status();
+}
 
 // b [K][N] fp32 (ld ldb)  ->  out [ceil(K/16)][3][N][16] bf16 split terms (k >= K zero-filled)
 __global__ void split_bf16x3_kernel(const float* __restrict__ b, long long ldb, int K, int N, __bf16* __restrict__ out) {
@@ -663,6 +861,12 @@ CDM_API int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int
     MkPre mb{reinterpret_cast<const __bf16*>(wx3), Cout};
     EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout};
     hipStream_t st = S(stream);
+    if (kc == 16 && W == H && (W == 64 || W == 32) && ldx % 4 == 0 && (H * W) % HBM_ == 0) {   // LDS-halo path
+        const EpiStoreW<4> eh{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout};
+        const __bf16* b = reinterpret_cast<const __bf16*>(wx3);
+        return W == 64 ? launch_conv_halo<64>(x, N, H, Cin, ldx, b, Cout, eh, nterm, st)
+                       : launch_conv_halo<32>(x, N, H, Cin, ldx, b, Cout, eh, nterm, st);
+    }
     if (Cin == 128 && Cout == 128 && H == 64 && W == 64 && kc == 16) {
         using LA = LdIm2colA<128, 16, 64>;
         return launch_gemm_x3<RowK<LA>::template T, StagePre, EpiStore, true>(MkRowK<LA>{LA{x, H, W, Cin, ldx, M, K}}, mb,
