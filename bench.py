@@ -248,8 +248,8 @@ def main():
                        "n_per_gpu": n, "guide_w": 0.0, "ms_per_denoise_step": round(dts / S * 1e3, 3),
                        "scaling": "replicas"},
             "roofline": {"bound": "mfma",
-                         "kernel": "conv3x3 128->128 @64x64 fwd (" + ("gemm_x3_kernel<StageRowK<LdIm2colA<128,16,64>>,"
-                                   "StagePre>" if CONV_MATH_INFO[args.conv_math][0] else
+                         "kernel": "conv3x3 128->128 @64x64 fwd (" + ("conv3x3_halo_x3_kernel<6,64>"
+                                   if CONV_MATH_INFO[args.conv_math][0] else
                                    "gemm_f32_kernel<LdIm2colA<128,16,64>>") + ")",
                          "arithmetic": CONV_MATH_INFO[args.conv_math][1],
                          "achieved": round(conv_tflops, 2), "peak": round(peak, 2), "unit": "TFLOP/s",

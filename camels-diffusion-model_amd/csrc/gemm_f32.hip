@@ -703,32 +703,43 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
             const __bf16* b = Bs + bb * BPL * XPLANE;
 #pragma unroll
             for (int dx = 0; dx < 3; ++dx) {
+                // term-major: the hi fragments are read first and the hh products issue while the mid / lo
+                // fragments are still in flight
                 bf16x8 fa[2][NS], fb[2][NS];
+                int ao[2];
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const int ao = xoff(hp0[i] + dy * HC + dx, kh);
+                for (int i = 0; i < 2; ++i) ao[i] = xoff(hp0[i] + dy * HC + dx, kh);
 #pragma unroll
-                    for (int t = 0; t < NS; ++t) {
-                        fa[i][t] = *reinterpret_cast<const bf16x8*>(a + t * HPLANE + ao);
+                for (int t = 0; t < NS; ++t)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        fa[i][t] = *reinterpret_cast<const bf16x8*>(a + t * HPLANE + ao[i]);
                         fb[i][t] = *reinterpret_cast<const bf16x8*>(b + (dx * NS + t) * XPLANE + boff[i]);
                     }
-                }
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        f32x16 c = acc[i][j];
-                        if constexpr (NT >= 6) {
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+                if constexpr (NT >= 3) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
                         }
-                        if constexpr (NT >= 3) {
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
-                            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+                }
+                if constexpr (NT >= 6) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
                         }
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
-                    }
+                }
             }
             if (moreg) store_b(Bs + (bb ^ 1) * BPL * XPLANE);
             if (dy == 0 && morec) store_halo(Hs + (hb ^ 1) * NS * HPLANE);   // buffer idle since chunk cc-1
@@ -738,6 +749,150 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         hb ^= 1;
     }
     ep(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
+}
+
+// ============================== conv3x3 weight gradient, split-bf16, transposed LDS reads ==============================
+// dW[co][tap*Cin + ci] (per split-K slab) = sum_pix dY[pix][co] * X[pix shifted by tap][ci]; K = pixels.
+// Both operands are stored pixel-major in HBM (channels contiguous), i.e. k-strided for the MFMA.  They
+// are staged exactly as they arrive — float4 along channels, split into bf16 terms, one [16 pix][128 ch]
+// image per term (256-byte rows, 16-byte chunks XOR-swizzled by row: conflict-free stores and reads) —
+// and the k-contiguous MFMA fragments are produced by the hardware transpose read ds_read_b64_tr_b16
+// (two per fragment).  Block: 128 co x 128 columns of one tap (Cin % 128 == 0, Cout % 128 == 0), 4 waves
+// 2x2 of 64x64, split-K over blockIdx.z.  The 16 pixels of a K step lie in one image row (W % 16 == 0),
+// so the tap shift is one bounds test per pixel.
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+static __device__ __forceinline__ int trswz(int row, int ch) {   // byte offset of 16-B chunk ch in row
+    return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+}
+
+template <int NT>
+__global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float* __restrict__ dy, int lddy, int Cout,
+                                                                     const float* __restrict__ x, int H, int W, int Cin,
+                                                                     int ldx, int K, int kt_per_split, EpiStore ep) {
+    constexpr int NS = XTerms<NT>::NS;
+    constexpr int IMG = 16 * 128;                     // bf16 per [16 pix][128 ch] term image
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * NS * IMG];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // 1-D grid, split-major logical order L = z*T + tile, remapped so that each XCD (hardware block b -> XCD b%8)
+    // runs a contiguous range of L: the T tiles of one split share their dY / X pixel range in that XCD's L2.
+    const int gx = Cout / GBM, T = gx * (9 * Cin / GBN);
+    int L;
+    {
+        const int nwg = gridDim.x, q8 = nwg >> 3, r8 = nwg & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+        L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + j;
+    }
+    const int bz = L / T, tl = L - bz * T;
+    const int m0 = (tl % gx) * GBM, n0 = (tl / gx) * GBN;
+    const int tap = n0 / Cin, ci0 = n0 - tap * Cin;
+    const int ky = tap / 3, sdy = ky - 1, sdx = tap - ky * 3 - 1;
+    const int ktiles = K / 16;
+    const int kt0 = bz * kt_per_split;
+    const int kt1 = min(ktiles, kt0 + kt_per_split);
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // staging map: thread -> pixel rows kk = (tid>>5) + 8i, channel quad c4 = (tid&31)*4
+    const int kq = tid >> 5, c4 = (tid & 31) * 4;
+    const int hw = H * W;
+    // running image coordinates of the K step's first pixel
+    int p0 = kt0 * 16;
+    int pn = p0 / hw, ph = (p0 - pn * hw) / W, pw = p0 - pn * hw - ph * W;
+    float4 ra[2], rb[2];
+    auto gload = [&]() {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int kk = kq + 8 * i;
+            const long long pix = (long long)(pn * H + ph) * W + pw + kk;
+            ra[i] = ld4(dy + pix * lddy + m0 + c4);
+            const int hh = ph + sdy, ww = pw + kk + sdx;
+            rb[i] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                        ? ld4(x + ((long long)(pn * H + hh) * W + ww) * ldx + ci0 + c4)
+                        : f4zero();
+        }
+        pw += 16;
+        if (pw >= W) { pw = 0; if (++ph == H) { ph = 0; ++pn; } }
+    };
+    auto sstore = [&](__bf16* base) {
+#pragma unroll
+        for (int op = 0; op < 2; ++op)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const float4 v = op ? rb[i] : ra[i];
+                const float xv[4] = {v.x, v.y, v.z, v.w};
+                __bf16 h[4], m[4], l[4];
+                split_terms<NS>(xv, h, m, l);
+                const int kk = kq + 8 * i;
+                char* d = reinterpret_cast<char*>(base + op * NS * IMG) + trswz(kk, c4 >> 3) + (c4 & 7) * 2;
+                *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
+                if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + IMG * 2) = bf16x4{m[0], m[1], m[2], m[3]};
+                if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + IMG * 4) = bf16x4{l[0], l[1], l[2], l[3]};
+            }
+    };
+    // transposed-read addresses: lane 4q+p of 16-lane group g supplies row kb+q, columns c0+4p..+3
+    const int g = (lane >> 4) & 3, q = (lane >> 2) & 3, pq = lane & 3;
+    const int kb = 8 * (g >> 1) + q;
+    int aoff[2][2], boff[2][2];   // [i][half] byte offsets within a term image
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ca = wm * 64 + 32 * i + 16 * (g & 1) + 4 * pq, cb = wn * 64 + 32 * i + 16 * (g & 1) + 4 * pq;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            aoff[i][hf] = trswz(kb + 4 * hf, ca >> 3) + (ca & 7) * 2;
+            boff[i][hf] = trswz(kb + 4 * hf, cb >> 3) + (cb & 7) * 2;
+        }
+    }
+
+    if (kt0 < kt1) { gload(); sstore(smem); }
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) gload();
+        const char* a = reinterpret_cast<const char*>(smem + cur * 2 * NS * IMG);
+        const char* b = a + NS * IMG * 2;
+        bf16x8 fa[2][NS], fb[2][NS];
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + t * IMG * 2 + aoff[i][0]));
+                const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + t * IMG * 2 + aoff[i][1]));
+                const bf16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(b + t * IMG * 2 + boff[i][0]));
+                const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(b + t * IMG * 2 + boff[i][1]));
+                fa[i][t] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+                fb[i][t] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x16 c = acc[i][j];
+                if constexpr (NT >= 6) {
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+                }
+                if constexpr (NT >= 3) {
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+                }
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+            }
+        if (more) sstore(smem + (cur ^ 1) * 2 * NS * IMG);
+        __syncthreads();
+        cur ^= 1;
+    }
+    EpiStore e = ep;                       // this block's split slab (the epilogue would index blockIdx.z)
+    e.y += (long long)bz * ep.zstride;
+    e.zstride = 0;
+    e(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
 }
 
 template <int WT>
@@ -889,6 +1044,22 @@ CDM_API int cdm_conv3x3_wgrad_x3(const float* dy, int lddy, int Cout, const floa
     const int M = Cout, NN = 9 * Cin, K = N * H * W;
     const int sp = effective_splits(K, splits);
     EpiStore ep{slab, NN, (long long)M * NN, nullptr, 1, 0, nullptr, 0, M, NN};
+    if (Cin % 128 == 0 && Cout % 128 == 0 && W % 16 == 0 && lddy % 4 == 0 && ldx % 4 == 0 &&
+        effective_splits(K, splits, 16) == sp) {   // transposed-read path
+        const int ktiles = K / 16, per = (ktiles + sp - 1) / sp;
+        dim3 grid((M / GBM) * (NN / GBN) * ((ktiles + per - 1) / per));
+        hipStream_t st = S(stream);
+        switch (nterm) {
+            case 1: hipLaunchKernelGGL(wgrad3x3_tr_x3_kernel<1>, grid, dim3(GTHREADS), 0, st, dy, lddy, Cout, x, H, W, Cin,
+                                       ldx, K, per, ep); break;
+            case 3: hipLaunchKernelGGL(wgrad3x3_tr_x3_kernel<3>, grid, dim3(GTHREADS), 0, st, dy, lddy, Cout, x, H, W, Cin,
+                                       ldx, K, per, ep); break;
+            case 6: hipLaunchKernelGGL(wgrad3x3_tr_x3_kernel<6>, grid, dim3(GTHREADS), 0, st, dy, lddy, Cout, x, H, W, Cin,
+                                       ldx, K, per, ep); break;
+            default: return (int)hipErrorInvalidValue;
+        }
+        return cdm_status();
+    }
     return launch_gemm_x3<ColK<LdDenseAT>::template T, ColK<LdIm2colB>::template T, EpiStore, false>(
         MkColK<LdDenseAT>{LdDenseAT{dy, lddy, M, K}}, MkColK<LdIm2colB>{LdIm2colB{x, H, W, Cin, ldx, K, NN}}, ep, M, NN,
         K, sp, nterm, S(stream));

@@ -106,7 +106,8 @@ def main():
         for shp, (x, w, wx, b, y) in bufs.items():
             B, H, ci, co = shp
             flops = 2.0 * B * H * H * ci * co * 9
-            sp = L.raw("cdm_gemm_splits")(B * H * H, 8)
+            tiles = -(-co // 128) * -(-(9 * ci) // 128)            # engine.wgrad_splits: ~2048 workgroups
+            sp = L.raw("cdm_gemm_splits")(B * H * H, max(1, min(512, -(-2048 // tiles))))
             slab = slabs.setdefault(shp, torch.empty(sp, co, 9 * ci, device="cuda"))
             for mode in modes:
                 wgrad(mode, y, x, B, H, ci, co, slab, sp)

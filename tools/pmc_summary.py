@@ -13,7 +13,7 @@ for f in sorted(glob.glob(os.path.join(root, "p*", "conv_counter_collection.csv"
     names = {}
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "gemm" not in k and "conv3x3" not in k:
+        if ("gemm" not in k and "conv3x3" not in k) or "pack" in k:
             continue
         agg[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
         names[r["Dispatch_Id"]] = k
