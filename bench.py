@@ -10,7 +10,10 @@ Metric (BASELINE.json): train-step images/s + T=1500 sample images/s, 64x64x1, b
             (+ bucketed RCCL gradient all-reduce when N > 1), n_feat=128, 6 params, fp32, synthetic data.
   sample  = T=1500 reverse diffusion of 256 images per GPU (w=0, hipGraph-captured steps, on-device
             snapshots): images / wall time; replicas only when N > 1 (no collective).
-  roofline: the dominant kernel (conv3x3 128->128 @64x64, fp32 MFMA) timed live with HIP events.
+            + CFG (w=1, 3: cond + uncond halves in one batched forward) over --cfg-sample-steps, extrapolated.
+  roofline: the dominant kernel (conv3x3 128->128 @64x64) timed live with HIP events on its stream.
+  configs (N=1 only): C4 = bf16 mixed-precision train + CFG w in {0,1,3} sampling; C5 = 256x256,
+            n_feat=256, T=2000 at --c5-batch (shortened runs, step counts in the output).
   cpu_baseline: the CPU oracle restatement (torch CPU fp32, the reference algorithm) on the host cores.
 """
 from __future__ import annotations
@@ -35,7 +38,10 @@ PEAK_BF16_TFLOPS = 2500.0               # MI355X dense bf16 MFMA (no sparsity)
 # conv arithmetic -> (bf16 MFMA products per fp32 MAC, description); peak = fp32-equivalent FLOP/s ceiling
 CONV_MATH_INFO = {"fp32": (0, "fp32 MFMA v_mfma_f32_32x32x2_f32"),
                   "x6": (6, "fp32-accurate split-bf16: 3-term bf16 operands, 6 cross products on "
-                            "v_mfma_f32_32x32x16_bf16, fp32 accumulate")}
+                            "v_mfma_f32_32x32x16_bf16, fp32 accumulate"),
+                  "h3": (3, "fp32-class split-fp16: operands scaled by a per-tensor power of two, 2-term fp16 "
+                            "(11+11 bits), 3 cross products on v_mfma_f32_32x32x16_f16, fp32 accumulate")}
+NT_CODE = {"fp32": 0, "x6": 6, "h3": 4}   # engine / C-ABI arithmetic code
 
 
 def _dist_env():
@@ -64,12 +70,21 @@ def time_dominant_conv(B: int, math: str, reps: int = 20):
                        16, s.cuda_stream)
     y = torch.empty(B * H * H, NF, device="cuda")
     stats = torch.empty((B * H * H + 127) // 128, 2, NF, device="cuda")
-    nterm = CONV_MATH_INFO[math][0]
+    nterm = NT_CODE[math]
     wx = torch.empty(9 * NF // 16 * 3 * NF * 16, dtype=torch.bfloat16, device="cuda")
-    L.cdm_split_bf16x3(wpk.data_ptr(), NF, 9 * NF, NF, wx.data_ptr(), s.cuda_stream)
+    am = torch.empty(2, device="cuda")
+    if nterm == 4:
+        L.cdm_amax_f32(wpk.data_ptr(), 9 * NF, NF, NF, am.data_ptr() + 4, 0, s.cuda_stream)
+        L.cdm_split_f16x2(wpk.data_ptr(), NF, 9 * NF, NF, am.data_ptr() + 4, wx.data_ptr(), s.cuda_stream)
+    else:
+        L.cdm_split_bf16x3(wpk.data_ptr(), NF, 9 * NF, NF, wx.data_ptr(), s.cuda_stream)
+    L.cdm_amax_f32(x.data_ptr(), B * H * H, NF, NF, am.data_ptr(), 0, s.cuda_stream)
 
     def launch():
-        if nterm:
+        if nterm == 4:
+            L.cdm_conv3x3_fwd_h3(x.data_ptr(), B, H, H, NF, NF, wx.data_ptr(), am.data_ptr(), am.data_ptr() + 4,
+                                 b.data_ptr(), y.data_ptr(), NF, NF, 0, stats.data_ptr(), NF, 16, s.cuda_stream)
+        elif nterm:
             L.cdm_conv3x3_fwd_x3(x.data_ptr(), B, H, H, NF, NF, wx.data_ptr(), b.data_ptr(), y.data_ptr(), NF, NF, 0,
                                  stats.data_ptr(), NF, 16, nterm, s.cuda_stream)
         else:
@@ -146,67 +161,14 @@ def cpu_baseline(threads: int):
     }
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--sample-steps", type=int, default=T, help="sampling steps actually run (T=1500 = full)")
-    ap.add_argument("--sample-batch", type=int, default=256)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--conv-math", choices=sorted(CONV_MATH_INFO), default="x6",
-                    help="3x3 conv arithmetic (both fp32-accurate; see DESIGN.md §3)")
-    args = ap.parse_args()
-
-    world, rank, local = _dist_env()
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    import cdm_amd
-    from cdm_amd import ContextUnet, Trainer
+def sample_rate(model, T: int, n: int, w: float, steps: int, rank: int, barrier, dist=None):
+    """Time `steps` hipGraph-replayed denoise steps (n images, guide weight w) -> (ms/step, steps run)."""
     from cdm_amd.diffusion import GraphSampler, Schedule
-
-    B = args.batch
-    torch.manual_seed(0)
-    model = ContextUnet(1, NF, NCF, H, shortcut_source="device", conv_math=args.conv_math).cuda()
-    trainer = Trainer(model, 1e-5, T, B, seed=rank, use_graph=not args.no_graph)
-    g = torch.Generator(device="cuda").manual_seed(1234 + rank)
-    x0 = torch.rand(B, 1, H, H, device="cuda", generator=g)   # synthetic maps in [0,1) (min-max range)
-    c = torch.rand(B, NCF, device="cuda", generator=g)        # synthetic normalised parameters
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        trainer.step(x0, c)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        trainer.step(x0, c)
-    barrier()
-    dt = time.perf_counter() - t0
-    loss = float(trainer.loss.item())
-    if dist is not None:
-        tt = torch.tensor([dt], device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    ms_step = dt / args.steps * 1e3
-    train_ips = world * B * args.steps / dt
-
-    # ---------------- sampling (replicas) ----------------
-    model.eval()
-    n = args.sample_batch
-    S = min(args.sample_steps, T)
+    H, ncf = model.h, model.n_cfeat
+    S = min(steps, T)
     sched = Schedule(T, "cuda")
-    params = torch.rand(n, NCF, generator=torch.Generator().manual_seed(77 + rank))
-    smp = GraphSampler(model, sched, n, 0.0, params, save_rate=20, z_source="device", seed=4321 + rank)
+    params = torch.rand(n, ncf, generator=torch.Generator().manual_seed(77 + rank))
+    smp = GraphSampler(model, sched, n, w, params, save_rate=20, z_source="device", seed=4321 + rank)
     smp.prepare_rng(host_z=False)
     x_T = torch.randn(n, 1, H, H, generator=torch.Generator().manual_seed(99 + rank))
     smp.prepare()                               # weight pack + hipGraph capture outside the timed region
@@ -219,11 +181,126 @@ def main():
         tt = torch.tensor([dts], device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dts = float(tt.item())
-    sample_ips = world * n / (dts * T / S)
+    del smp
+    return dts / S * 1e3, S
+
+
+def train_rate(nf: int, H: int, T: int, B: int, math: str, steps: int, warmup: int, rank: int, barrier,
+               use_graph: bool = True, dist=None):
+    """Train steps/s of a fresh seeded ContextUnet on synthetic data -> (model, ms/step, final loss)."""
+    from cdm_amd import ContextUnet, Trainer
+    torch.manual_seed(0)
+    model = ContextUnet(1, nf, NCF, H, shortcut_source="device", conv_math=math).cuda()
+    trainer = Trainer(model, 1e-5, T, B, seed=rank, use_graph=use_graph)
+    g = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    x0 = torch.rand(B, 1, H, H, device="cuda", generator=g)   # synthetic maps in [0,1) (min-max range)
+    c = torch.rand(B, NCF, device="cuda", generator=g)        # synthetic normalised parameters
+    for _ in range(warmup):
+        trainer.step(x0, c)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        trainer.step(x0, c)
+    barrier()
+    dt = time.perf_counter() - t0
+    loss = float(trainer.loss.item())
+    if dist is not None:
+        tt = torch.tensor([dt], device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    del trainer
+    model.eval()
+    return model, dt / steps * 1e3, loss
+
+
+def extra_configs(args, barrier):
+    """BASELINE configs C4 (bf16 mixed-precision train + CFG sampling) and C5 (256x256, n_feat=256, T=2000),
+    single GPU, shortened runs (step counts stated in the output)."""
+    out = {}
+    # C4: bf16 MFMA operands, fp32 accumulate / master weights / activations; CFG w in {0,1,3}
+    model, ms, loss = train_rate(NF, H, T, args.batch, "bf16", 10, 3, 0, barrier)
+    c4 = {"workload": "C4: ContextUnet n_feat=128 64x64, bf16 mixed-precision convs (bf16 operands, fp32 "
+                      "accumulate, fp32 master weights / activations / norms), T=1500",
+          "batch": args.batch, "train_img_per_s": round(args.batch / (ms * 1e-3), 2), "train_ms_per_step": round(ms, 3),
+          "train_steps": 10, "final_loss": loss, "sample": {}}
+    for w in (0.0, 1.0, 3.0):
+        sms, S = sample_rate(model, T, args.sample_batch, w, args.extra_sample_steps, 0, barrier)
+        c4["sample"][f"w={w:g}"] = {"ms_per_denoise_step": round(sms, 3), "steps_run": S,
+                                   "img_per_s": round(args.sample_batch / (sms * 1e-3 * T), 4),
+                                   "extrapolated_to_T": S < T}
+    out["c4_bf16_cfg"] = c4
+    del model
+    torch.cuda.empty_cache()
+    # C5: 256x256 maps, n_feat=256 (1.093 B params; up0 alone 1.07 B), T=2000, split-bf16 fp32-accurate convs
+    B5, T5 = args.c5_batch, 2000
+    model, ms, loss = train_rate(256, 256, T5, B5, args.conv_math, 3, 1, 0, barrier)
+    sms, S = sample_rate(model, T5, B5, 0.0, 20, 0, barrier)
+    out["c5_256"] = {"workload": "C5: ContextUnet n_feat=256, 256x256x1, 6 params, T=2000, train-mode BatchNorm",
+                     "conv_math": args.conv_math, "batch": B5, "train_img_per_s": round(B5 / (ms * 1e-3), 3),
+                     "train_ms_per_step": round(ms, 3), "train_steps": 3, "final_loss": loss,
+                     "train_tflops": round(3 * 1226.82 * B5 / ms, 2),
+                     "sample": {"w=0": {"ms_per_denoise_step": round(sms, 3), "steps_run": S,
+                                        "img_per_s": round(B5 / (sms * 1e-3 * T5), 5), "extrapolated_to_T": True}}}
+    del model
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--sample-steps", type=int, default=T, help="sampling steps actually run (T=1500 = full)")
+    ap.add_argument("--sample-batch", type=int, default=256)
+    ap.add_argument("--cfg-sample-steps", type=int, default=100,
+                    help="steps run for the C2 CFG (w=1,3) sampling rates (extrapolated to T)")
+    ap.add_argument("--extra-sample-steps", type=int, default=100, help="sampling steps of the C4 legs")
+    ap.add_argument("--c5-batch", type=int, default=16)
+    ap.add_argument("--no-extra", action="store_true", help="skip the C4 / C5 legs")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--conv-math", choices=sorted(CONV_MATH_INFO), default="x6",
+                    help="3x3 conv arithmetic of the C2 / C5 legs (fp32-accurate; see DESIGN.md §3)")
+    args = ap.parse_args()
+
+    world, rank, local = _dist_env()
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import cdm_amd  # noqa: F401
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    B = args.batch
+    model, ms_step, loss = train_rate(NF, H, T, B, args.conv_math, args.steps, args.warmup, rank, barrier,
+                                      use_graph=not args.no_graph, dist=dist)
+    train_ips = world * B / (ms_step * 1e-3)
+
+    # ---------------- sampling (replicas) ----------------
+    n = args.sample_batch
+    sms, S = sample_rate(model, T, n, 0.0, args.sample_steps, rank, barrier, dist)
+    sample_ips = world * n / (sms * 1e-3 * T)
+    cfg = {}
+    for w in (1.0, 3.0):
+        cms, CS = sample_rate(model, T, n, w, args.cfg_sample_steps, rank, barrier, dist)
+        cfg[f"w={w:g}"] = {"ms_per_denoise_step": round(cms, 3), "steps_run": CS,
+                           "img_per_s": round(world * n / (cms * 1e-3 * T), 4), "extrapolated_to_T": CS < T}
+    del model
+    torch.cuda.empty_cache()
 
     # ---------------- roofline of the dominant kernel ----------------
     conv_ms, conv_tflops = time_dominant_conv(B, args.conv_math)
     peak = conv_peak(args.conv_math)
+
+    extra = extra_configs(args, barrier) if (world == 1 and not args.no_extra) else None
 
     out = None
     if rank == 0:
@@ -245,24 +322,26 @@ def main():
                        "batch_per_gpu": B, "global_batch": B * world, "n_feat": NF, "n_cfeat": NCF, "T": T,
                        "parallelism": f"dp{world}", "conv_math": args.conv_math},
             "sample": {"img_per_s": round(sample_ips, 4), "T": T, "steps_run": S, "extrapolated": S < T,
-                       "n_per_gpu": n, "guide_w": 0.0, "ms_per_denoise_step": round(dts / S * 1e3, 3),
-                       "scaling": "replicas"},
+                       "n_per_gpu": n, "guide_w": 0.0, "ms_per_denoise_step": round(sms, 3),
+                       "scaling": "replicas", "cfg": cfg},
             "roofline": {"bound": "mfma",
-                         "kernel": "conv3x3 128->128 @64x64 fwd (" + ("conv3x3_halo_x3_kernel<6,64>"
-                                   if CONV_MATH_INFO[args.conv_math][0] else
-                                   "gemm_f32_kernel<LdIm2colA<128,16,64>>") + ")",
+                         "kernel": "conv3x3 128->128 @64x64 fwd (" + (
+                             f"conv3x3_halo_x3_kernel<{NT_CODE[args.conv_math]},64>" if NT_CODE[args.conv_math]
+                             else "gemm_f32_kernel<LdIm2colA<128,16,64>>") + ")",
                          "arithmetic": CONV_MATH_INFO[args.conv_math][1],
                          "achieved": round(conv_tflops, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
                          "frac": round(conv_tflops / peak, 4), "traffic": pmc_traffic(args.conv_math),
                          "launch_ms": round(conv_ms, 4),
                          "algorithmic": f"{CONV_GFLOP_PER_IMG} GFLOP/img x {B} img per launch (fp32 FLOPs); peak = "
                                         + ("fp32 MFMA dense" if peak == PEAK_FP32_TFLOPS else
-                                           f"bf16 MFMA dense {PEAK_BF16_TFLOPS:.0f} / "
+                                           f"bf16/fp16 MFMA dense {PEAK_BF16_TFLOPS:.0f} / "
                                            f"{CONV_MATH_INFO[args.conv_math][0]} products per fp32 MAC"),
                          "vs_fp32_mfma_peak": round(conv_tflops / PEAK_FP32_TFLOPS, 4)},
             "train_tflops_per_gpu": round(3 * FWD_GFLOP_PER_IMG * B / (ms_step * 1e-3) / 1e3, 2),
             "final_loss": loss,
         }
+        if extra:
+            out["configs"] = extra
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
         print(json.dumps(out), flush=True)
