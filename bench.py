@@ -83,7 +83,7 @@ def time_dominant_conv(B: int, math: str, reps: int = 20):
     def launch():
         if nterm == 4:
             L.cdm_conv3x3_fwd_h3(x.data_ptr(), B, H, H, NF, NF, wx.data_ptr(), am.data_ptr(), am.data_ptr() + 4,
-                                 b.data_ptr(), y.data_ptr(), NF, NF, 0, stats.data_ptr(), NF, 16, s.cuda_stream)
+                                 b.data_ptr(), y.data_ptr(), NF, NF, 0, stats.data_ptr(), NF, 16, None, s.cuda_stream)
         elif nterm:
             L.cdm_conv3x3_fwd_x3(x.data_ptr(), B, H, H, NF, NF, wx.data_ptr(), b.data_ptr(), y.data_ptr(), NF, NF, 0,
                                  stats.data_ptr(), NF, 16, nterm, s.cuda_stream)
@@ -262,7 +262,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--conv-math", choices=sorted(CONV_MATH_INFO), default="x6",
+    ap.add_argument("--conv-math", choices=sorted(CONV_MATH_INFO), default="h3",
                     help="3x3 conv arithmetic of the C2 / C5 legs (fp32-accurate; see DESIGN.md §3)")
     args = ap.parse_args()
 

@@ -35,3 +35,24 @@ static __device__ __forceinline__ float wave_sum(float v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+
+static __device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// *out = max(*out, block max of m) for non-negative m (atomic max on the float's bits).  Every thread of
+// the block must call it (it synchronises the block).  Producers use it to hand the h3 convolutions the
+// max|.| of the tensor they write (csrc/gemm_f32.hip, NT_H3) without a separate pass over it.
+static __device__ __forceinline__ void block_amax_commit(float m, float* out) {
+    __shared__ float red[16];
+    m = wave_max(m);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) red[w] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)((blockDim.x + 63) >> 6); ++i) m = fmaxf(m, red[i]);
+        atomicMax(reinterpret_cast<unsigned*>(out), __float_as_uint(m));
+    }
+}

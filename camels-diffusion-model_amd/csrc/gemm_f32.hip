@@ -169,22 +169,44 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
     float* y; long long ldy; long long zstride; const float* bias; int bias_mod; int flags;
     float* stats; int stats_ld;  // stats[tile][0|1][stats_ld]: sum / sum of squares of the stored value
     int M, N;
+    float* amax = nullptr;       // optional running max|stored value| (block_amax_commit)
 
     __device__ __forceinline__ void operator()(f32x16 (&acc)[2][2], int mw, int nw, int lane, int wm, int wn,
                                                float* scratch, int tid) const {
         float* yz = y + (long long)blockIdx.z * zstride;
         float cs[2] = {0.f, 0.f}, cq[2] = {0.f, 0.f};
-        CDM_FOR_ACC({
-            if (m < M && n < N) {
-                float v = acc[i][j][r];
-                if (bias) v += bias[n % bias_mod];
-                float* p = yz + (long long)m * ldy + n;
-                if (flags & EPI_ACCUM) v += *p;
-                if (flags & EPI_RELU) v = fmaxf(v, 0.f);
-                *p = v;
+        float am = 0.f;
+        if (mw - wm * 64 + WM * 64 <= M && (nw - wn * 64) + GBN <= N) {
+            // whole block tile in range (the hot shapes): no per-element bounds branches, bias hoisted (one
+            // column per lane and j)
+            float bj[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bj[j] = bias ? bias[(nw + 32 * j + (lane & 31)) % bias_mod] : 0.f;
+            const bool relu = flags & EPI_RELU;
+            const bool accum = flags & EPI_ACCUM;
+            CDM_FOR_ACC({
+                float v = acc[i][j][r] + bj[j];
+                if (accum) v += yz[(long long)m * ldy + n];
+                if (relu) v = fmaxf(v, 0.f);
+                yz[(long long)m * ldy + n] = v;
                 cs[j] += v; cq[j] += v * v;
-            }
-        })
+                am = fmaxf(am, fabsf(v));
+            })
+        } else {
+            CDM_FOR_ACC({
+                if (m < M && n < N) {
+                    float v = acc[i][j][r];
+                    if (bias) v += bias[n % bias_mod];
+                    float* p = yz + (long long)m * ldy + n;
+                    if (flags & EPI_ACCUM) v += *p;
+                    if (flags & EPI_RELU) v = fmaxf(v, 0.f);
+                    *p = v;
+                    cs[j] += v; cq[j] += v * v;
+                    am = fmaxf(am, fabsf(v));
+                }
+            })
+        }
+        if (amax) block_amax_commit(am, amax);
         if (!stats) return;
 #pragma unroll
         for (int j = 0; j < 2; ++j) { cs[j] += __shfl_xor(cs[j], 32, 64); cq[j] += __shfl_xor(cq[j], 32, 64); }
@@ -213,8 +235,10 @@ using EpiStore = EpiStoreW<2>;
 
 struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n, 2h+i, 2w+j, co] = acc + b[co]
     float* y; long long ldy; const float* bias; int H, W, Co, M, N;
+    float* amax = nullptr;       // optional running max|y| (block_amax_commit)
     __device__ __forceinline__ void operator()(f32x16 (&acc)[2][2], int mw, int nw, int lane, int, int,
                                                float*, int) const {
+        float am = 0.f;
         CDM_FOR_ACC({
             if (m < M && n < N) {
                 const int hw = H * W; const int b = m / hw; const int rem = m - b * hw;
@@ -222,8 +246,10 @@ struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n,
                 const int ij = n / Co, co = n - ij * Co;
                 float v = acc[i][j][r] + (bias ? bias[co] : 0.f);
                 y[((long long)(b * 2 * H + 2 * h + (ij >> 1)) * (2 * W) + 2 * w + (ij & 1)) * ldy + co] = v;
+                am = fmaxf(am, fabsf(v));
             }
         })
+        if (amax) block_amax_commit(am, amax);
     }
 };
 
@@ -352,6 +378,15 @@ static int effective_splits(int K, int splits, int BK = 16) {
 //   NT = 6: mm, lh, hl, mh, hm, hh    (dropped: ml, lm, ll <= 2^-24 |ab|  -> fp32-class error)
 //   NT = 3: mh, hm, hh                (~2^-16 relative; bf16x3)
 //   NT = 1: hh                        (plain bf16 operands, fp32 accumulate)
+//   NT = 4 (NT_H3): fp16 two-term split, 3 products on v_mfma_f32_32x32x16_f16 (fp32-class, see below)
+// NT_H3: x is first scaled by a per-tensor power of two s = 2^(14 - e), max|x| < 2^e (exact), so the
+// whole tensor sits inside fp16's normal range, then x*s = hi + lo + O(2^-22 |x*s|) with hi = f16(x*s),
+// lo = f16(x*s - hi): 11 + 11 significand bits.  a.b ~ hh + hl + lh (dropped ll <= 2^-22 |ab|); the
+// accumulator is multiplied back by 1/(s_a s_b) (exact).  Representation error per product is 2^-22
+// relative vs fp32's 2^-24 rounding of each product — below the fp32 accumulation error of a K >= 64
+// dot product — at half the matrix-core work of NT = 6.  max|x| comes from cdm_amax_f32 (device scalar,
+// read by the kernel: no host sync).  Elements < 2^-28 max|x| lose significand bits (fp16 subnormals);
+// their absolute error stays < 2^-39 max|x|.
 // v_mfma_f32_32x32x16_bf16 retires 16x the MACs of v_mfma_f32_32x32x2_f32 per cycle, so NT = 6 moves
 // 2.67x the fp32-MFMA rate through the matrix cores.
 // LDS images are [term][row][16 k] bf16, 32 bytes per row, no padding; the two 16-byte k-halves of a
@@ -366,6 +401,47 @@ static int effective_splits(int K, int splits, int BK = 16) {
 //              (lanes on consecutive rows -> coalesced), split, ds_write_b128 x terms
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int NT_H3 = 4;
+
+// the power-of-two operand scale of NT_H3 (1 for the bf16 arithmetics or a missing / degenerate max)
+template <int NT>
+static __device__ __forceinline__ float op_scale(const float* amax) {
+    if constexpr (NT != NT_H3) {
+        return 1.f;
+    } else {
+        if (!amax) return 1.f;
+        const float m = *amax;
+        if (!(m > 0.f) || m > 3.0e38f) return 1.f;
+        int e;
+        frexpf(m, &e);                               // m = f 2^e, f in [0.5, 1)  ->  m 2^(14-e) < 2^14
+        return ldexpf(1.f, min(126, max(-126, 14 - e)));
+    }
+}
+
+// one 32x32x16 product on the matrix cores in the arithmetic NT (operands are 16-bit images either way)
+template <int NT>
+static __device__ __forceinline__ f32x16 xmfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+    if constexpr (NT == NT_H3)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                      0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// acc *= 1 / (s_a s_b) for NT_H3 (two exact power-of-two multiplies)
+template <int NT>
+static __device__ __forceinline__ void unscale(f32x16 (&acc)[2][2], float sa, float sb) {
+    if constexpr (NT == NT_H3) {
+        const float ia = 1.f / sa, ib = 1.f / sb;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = (acc[i][j][r] * ia) * ib;
+    }
+}
 constexpr int XBK = 16;
 constexpr int XPLANE = GBM * XBK;     // elements per term plane (GBM == GBN == 128 rows x 16 k)
 
@@ -374,27 +450,42 @@ static __device__ __forceinline__ int xoff(int row, int k) {
     return row * XBK + ((((k >> 3) ^ (row >> 3)) & 1) << 3) + (k & 7);
 }
 
-template <int NS, int E>
-static __device__ __forceinline__ void split_terms(const float (&x)[E], __bf16 (&h)[E], __bf16 (&m)[E],
+template <int NT> struct XTerms { static constexpr int NS = NT >= 6 ? 3 : (NT >= 3 ? 2 : 1); };
+
+// x -> NS 16-bit terms (bf16 hi/mid/lo, or for NT_H3 the fp16 hi/lo of x * sc, bit-stored as __bf16)
+template <int NT, int E>
+static __device__ __forceinline__ void split_terms(const float (&x)[E], float sc, __bf16 (&h)[E], __bf16 (&m)[E],
                                                    __bf16 (&l)[E]) {
+    constexpr int NS = XTerms<NT>::NS;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        h[e] = (__bf16)x[e];
-        if constexpr (NS > 1) {
-            const float r = x[e] - (float)h[e];
-            m[e] = (__bf16)r;
-            if constexpr (NS > 2) l[e] = (__bf16)(r - (float)m[e]);
+        if constexpr (NT == NT_H3) {
+            const float v = x[e] * sc;
+            const _Float16 hi = (_Float16)v;
+            h[e] = __builtin_bit_cast(__bf16, hi);
+            m[e] = __builtin_bit_cast(__bf16, (_Float16)(v - (float)hi));
+        } else {
+            h[e] = (__bf16)x[e];
+            if constexpr (NS > 1) {
+                const float r = x[e] - (float)h[e];
+                m[e] = (__bf16)r;
+                if constexpr (NS > 2) l[e] = (__bf16)(r - (float)m[e]);
+            }
         }
     }
 }
 
-template <class LD, int NS>
+template <class LD, int NT>
 struct StageRowK {
+    static constexpr int NS = XTerms<NT>::NS;
     static constexpr int LDN = GBM * XBK / 4 / GTHREADS;   // 2 float4 per thread
     LD ld;
+    const float* amax;
+    float sc;
     typename LD::Row row[LDN];
     float4 r[LDN];
     __device__ __forceinline__ void init(int tid, int r0) {
+        sc = op_scale<NT>(amax);
 #pragma unroll
         for (int i = 0; i < LDN; ++i) row[i] = ld.row(r0 + tid / 4 + i * (GTHREADS / 4));
     }
@@ -407,7 +498,7 @@ struct StageRowK {
         for (int i = 0; i < LDN; ++i) {
             const float x[4] = {r[i].x, r[i].y, r[i].z, r[i].w};
             __bf16 h[4], m[4], l[4];
-            split_terms<NS>(x, h, m, l);
+            split_terms<NT>(x, sc, h, m, l);
             __bf16* d = base + xoff(tid / 4 + i * (GTHREADS / 4), (tid % 4) * 4);
             *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
             if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + XPLANE) = bf16x4{m[0], m[1], m[2], m[3]};
@@ -416,12 +507,18 @@ struct StageRowK {
     }
 };
 
-template <int NS>
+template <int NT>
 struct StagePre {
+    static constexpr int NS = XTerms<NT>::NS;
     const __bf16* p; int rows;           // [ktiles][3][rows][16]
+    const float* amax;                   // NT_H3: max|W| the terms were split with (cdm_split_f16x2)
+    float sc;
     int rr, kh; bool ok;
     uint4 r[NS];
-    __device__ __forceinline__ void init(int tid, int r0) { rr = r0 + (tid >> 1); kh = (tid & 1) * 8; ok = rr < rows; }
+    __device__ __forceinline__ void init(int tid, int r0) {
+        sc = op_scale<NT>(amax);
+        rr = r0 + (tid >> 1); kh = (tid & 1) * 8; ok = rr < rows;
+    }
     __device__ __forceinline__ void gload(int, int kt) {
 #pragma unroll
         for (int t = 0; t < NS; ++t)
@@ -435,17 +532,20 @@ struct StagePre {
     }
 };
 
-template <class LD, int NS>
+template <class LD, int NT>
 struct StageColK {
+    static constexpr int NS = XTerms<NT>::NS;
     LD ld;
+    const float* amax;
+    float sc;
     typename LD::Col col;
     float r[8];
     // thread -> (row tid>>1, k-half tid&1): an 8-lane store group covers 4 rows x 2 halves (conflict-free)
-    __device__ __forceinline__ void init(int tid, int r0) { col = ld.col(r0 + (tid >> 1)); }
+    __device__ __forceinline__ void init(int tid, int r0) { sc = op_scale<NT>(amax); col = ld.col(r0 + (tid >> 1)); }
     __device__ __forceinline__ void gload(int tid, int kt) { ld.load8(col, kt * XBK + (tid & 1) * 8, r); }
     __device__ __forceinline__ void sstore(int tid, __bf16* base) const {
         __bf16 h[8], m[8], l[8];
-        split_terms<NS>(r, h, m, l);
+        split_terms<NT>(r, sc, h, m, l);
         __bf16* d = base + xoff(tid >> 1, (tid & 1) * 8);
         *reinterpret_cast<bf16x8*>(d) = bf16x8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
         if constexpr (NS > 1)
@@ -454,8 +554,6 @@ struct StageColK {
             *reinterpret_cast<bf16x8*>(d + 2 * XPLANE) = bf16x8{l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7]};
     }
 };
-
-template <int NT> struct XTerms { static constexpr int NS = NT >= 6 ? 3 : (NT >= 3 ? 2 : 1); };
 
 // SA: operand A stager (rows = M), SB: operand B stager (rows = N); split-K over blockIdx.z.
 template <class SA, class SB, class EP, int NT, bool XCD_REMAP>
@@ -516,15 +614,15 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa, SB sb, EP e
             for (int j = 0; j < 2; ++j) {
                 f32x16 c = acc[i][j];
                 if constexpr (NT >= 6) {
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);   // mm
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);   // lh
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);   // hl
+                    c = xmfma<NT>(fa[i][1], fb[j][1], c);   // mm
+                    c = xmfma<NT>(fa[i][2], fb[j][0], c);   // lh
+                    c = xmfma<NT>(fa[i][0], fb[j][2], c);   // hl
                 }
                 if constexpr (NT >= 3) {
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);   // mh
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);   // hm
+                    c = xmfma<NT>(fa[i][1], fb[j][0], c);   // mh (NT_H3: lo.hi)
+                    c = xmfma<NT>(fa[i][0], fb[j][1], c);   // hm (NT_H3: hi.lo)
                 }
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);  // hh
+                acc[i][j] = xmfma<NT>(fa[i][0], fb[j][0], c);  // hh
             }
         if (more) {
             sa.sstore(tid, As + (cur ^ 1) * NS * XPLANE);
@@ -533,6 +631,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa, SB sb, EP e
         __syncthreads();
         cur ^= 1;
     }
+    unscale<NT>(acc, sa.sc, sb.sc);
     ep(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
 }
 
@@ -549,29 +648,32 @@ static int launch_gemm_x3(MkA mka, MkB mkb, const EP& ep, int M, int N, int K, i
     switch (nterm) {
         case 1: hipLaunchKernelGGL((gemm_x3_kernel<SAT<1>, SBT<1>, EP, 1, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
                                    mka.template make<1>(), mkb.template make<1>(), ep, K, per); break;
-        case 3: hipLaunchKernelGGL((gemm_x3_kernel<SAT<2>, SBT<2>, EP, 3, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
-                                   mka.template make<2>(), mkb.template make<2>(), ep, K, per); break;
-        case 6: hipLaunchKernelGGL((gemm_x3_kernel<SAT<3>, SBT<3>, EP, 6, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
+        case 3: hipLaunchKernelGGL((gemm_x3_kernel<SAT<3>, SBT<3>, EP, 3, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
                                    mka.template make<3>(), mkb.template make<3>(), ep, K, per); break;
+        case NT_H3: hipLaunchKernelGGL((gemm_x3_kernel<SAT<NT_H3>, SBT<NT_H3>, EP, NT_H3, XCD_REMAP>), grid,
+                                       dim3(GTHREADS), 0, s, mka.template make<NT_H3>(), mkb.template make<NT_H3>(), ep,
+                                       K, per); break;
+        case 6: hipLaunchKernelGGL((gemm_x3_kernel<SAT<6>, SBT<6>, EP, 6, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
+                                   mka.template make<6>(), mkb.template make<6>(), ep, K, per); break;
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();
 }
 
 template <class LD> struct MkRowK {
-    LD ld;
-    template <int NS> StageRowK<LD, NS> make() const { StageRowK<LD, NS> s; s.ld = ld; return s; }
+    LD ld; const float* amax = nullptr;
+    template <int NT> StageRowK<LD, NT> make() const { StageRowK<LD, NT> s; s.ld = ld; s.amax = amax; return s; }
 };
 template <class LD> struct MkColK {
-    LD ld;
-    template <int NS> StageColK<LD, NS> make() const { StageColK<LD, NS> s; s.ld = ld; return s; }
+    LD ld; const float* amax = nullptr;
+    template <int NT> StageColK<LD, NT> make() const { StageColK<LD, NT> s; s.ld = ld; s.amax = amax; return s; }
 };
 struct MkPre {
-    const __bf16* p; int rows;
-    template <int NS> StagePre<NS> make() const { StagePre<NS> s; s.p = p; s.rows = rows; return s; }
+    const __bf16* p; int rows; const float* amax = nullptr;
+    template <int NT> StagePre<NT> make() const { StagePre<NT> s; s.p = p; s.rows = rows; s.amax = amax; return s; }
 };
-template <class LD> struct RowK { template <int NS> using T = StageRowK<LD, NS>; };
-template <class LD> struct ColK { template <int NS> using T = StageColK<LD, NS>; };
+template <class LD> struct RowK { template <int NT> using T = StageRowK<LD, NT>; };
+template <class LD> struct ColK { template <int NT> using T = StageColK<LD, NT>; };
 
 // ============================== LDS-halo conv3x3 on the split-bf16 matrix cores ==============================
 // conv3x3 (stride 1, pad 1) forward / dgrad for Cin % 16 == 0 (channel-chunk-major K, kc = 16) and image
@@ -590,7 +692,8 @@ constexpr int HTHREADS = 512;
 template <int NT, int WT, class EP, bool XCD_REMAP>
 __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const float* __restrict__ x, int H, int Cin,
                                                                       int ldx, const __bf16* __restrict__ wx3,
-                                                                      int Cout, EP ep) {
+                                                                      int Cout, const float* amax_x,
+                                                                      const float* amax_w, EP ep) {
     constexpr int NS = XTerms<NT>::NS;
     constexpr int ROWS = HBM_ / WT, HR = ROWS + 2, HC = WT + 2, HPX = HR * HC;
     constexpr int HPLANE = HPX * XBK;                 // bf16 per halo term plane
@@ -611,6 +714,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     const int m0 = bx * HBM_, n0 = blockIdx.y * GBN;
     const int hw = H * WT, img = m0 / hw, h0 = (m0 - img * hw) / WT;
     const int nchunks = Cin / 16, ngroups = nchunks * 3;
+    const float sx = op_scale<NT>(amax_x);
 
     f32x16 acc[2][2];
 #pragma unroll
@@ -641,7 +745,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
             if (q < HPX * 4) {
                 const float xv[4] = {hreg[j].x, hreg[j].y, hreg[j].z, hreg[j].w};
                 __bf16 h[4], m[4], l[4];
-                split_terms<NS>(xv, h, m, l);
+                split_terms<NT>(xv, sx, h, m, l);
                 __bf16* d = base + xoff(q >> 2, (q & 3) * 4);
                 *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
                 if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + HPLANE) = bf16x4{m[0], m[1], m[2], m[3]};
@@ -650,8 +754,11 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         }
     };
     // ---- B staging: piece q = (plane q>>8 = dx*NS + t, col (q&255)>>1, k-half q&1) of group g ----
-    uint4 breg[BQ];
-    auto gload_b = [&](int g) {
+    // two register sets for B: the groups dy = 1 and dy = 2 of a chunk are both fetched at the chunk's start,
+    // ahead of the next chunk's halo, so the per-group B waits never wait for the (HBM-latency) halo loads:
+    // the halo has the whole chunk (3 barrier intervals) to arrive (vmcnt counts in issue order)
+    uint4 bregA[BQ], bregB[BQ];
+    auto gload_b = [&](int g, uint4 (&breg)[BQ]) {
 #pragma unroll
         for (int j = 0; j < BQ; ++j) {
             const int q = tid + j * HTHREADS;
@@ -663,7 +770,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
                           : make_uint4(0, 0, 0, 0);
         }
     };
-    auto store_b = [&](__bf16* base) {
+    auto store_b = [&](__bf16* base, const uint4 (&breg)[BQ]) {
 #pragma unroll
         for (int j = 0; j < BQ; ++j) {
             const int q = tid + j * HTHREADS;
@@ -685,69 +792,84 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 #pragma unroll
     for (int j = 0; j < 2; ++j) boff[j] = xoff(wn * 64 + 32 * j + (lane & 31), kh);
 
+    // the 3 taps (dx) of kernel row dy of the current chunk: fragments from the halo image a and B group b
+    auto compute = [&](int dy, const __bf16* a, const __bf16* b) {
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+            // term-major: the hi fragments are read first and the hh products issue while the mid / lo
+            // fragments are still in flight
+            bf16x8 fa[2][NS], fb[2][NS];
+            int ao[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) ao[i] = xoff(hp0[i] + dy * HC + dx, kh);
+#pragma unroll
+            for (int t = 0; t < NS; ++t)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    fa[i][t] = *reinterpret_cast<const bf16x8*>(a + t * HPLANE + ao[i]);
+                    fb[i][t] = *reinterpret_cast<const bf16x8*>(b + (dx * NS + t) * XPLANE + boff[i]);
+                }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = xmfma<NT>(fa[i][0], fb[j][0], acc[i][j]);
+            if constexpr (NT >= 3) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        acc[i][j] = xmfma<NT>(fa[i][0], fb[j][1], acc[i][j]);
+                        acc[i][j] = xmfma<NT>(fa[i][1], fb[j][0], acc[i][j]);
+                    }
+            }
+            if constexpr (NT >= 6) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        acc[i][j] = xmfma<NT>(fa[i][1], fb[j][1], acc[i][j]);
+                        acc[i][j] = xmfma<NT>(fa[i][0], fb[j][2], acc[i][j]);
+                        acc[i][j] = xmfma<NT>(fa[i][2], fb[j][0], acc[i][j]);
+                    }
+            }
+        }
+    };
+
     gload_halo(0);
-    gload_b(0);
+    gload_b(0, bregA);
     store_halo(Hs);
-    store_b(Bs);
+    store_b(Bs, bregA);
     __syncthreads();
     int hb = 0, bb = 0;
     for (int cc = 0; cc < nchunks; ++cc) {
         const bool morec = cc + 1 < nchunks;
+        const int g0 = cc * 3;
+        const __bf16* a = Hs + hb * NS * HPLANE;
+        // dy = 0: fetch B of dy = 1 and dy = 2, then the next chunk's halo
+        gload_b(g0 + 1, bregA);
+        gload_b(g0 + 2, bregB);
         if (morec) gload_halo(cc + 1);
-#pragma unroll 1
-        for (int dy = 0; dy < 3; ++dy) {
-            const int g = cc * 3 + dy;
-            const bool moreg = g + 1 < ngroups;
-            if (moreg) gload_b(g + 1);
-            const __bf16* a = Hs + hb * NS * HPLANE;
-            const __bf16* b = Bs + bb * BPL * XPLANE;
-#pragma unroll
-            for (int dx = 0; dx < 3; ++dx) {
-                // term-major: the hi fragments are read first and the hh products issue while the mid / lo
-                // fragments are still in flight
-                bf16x8 fa[2][NS], fb[2][NS];
-                int ao[2];
-#pragma unroll
-                for (int i = 0; i < 2; ++i) ao[i] = xoff(hp0[i] + dy * HC + dx, kh);
-#pragma unroll
-                for (int t = 0; t < NS; ++t)
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        fa[i][t] = *reinterpret_cast<const bf16x8*>(a + t * HPLANE + ao[i]);
-                        fb[i][t] = *reinterpret_cast<const bf16x8*>(b + (dx * NS + t) * XPLANE + boff[i]);
-                    }
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
-                if constexpr (NT >= 3) {
-#pragma unroll
-                    for (int i = 0; i < 2; ++i)
-#pragma unroll
-                        for (int j = 0; j < 2; ++j) {
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-                        }
-                }
-                if constexpr (NT >= 6) {
-#pragma unroll
-                    for (int i = 0; i < 2; ++i)
-#pragma unroll
-                        for (int j = 0; j < 2; ++j) {
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-                        }
-                }
-            }
-            if (moreg) store_b(Bs + (bb ^ 1) * BPL * XPLANE);
-            if (dy == 0 && morec) store_halo(Hs + (hb ^ 1) * NS * HPLANE);   // buffer idle since chunk cc-1
-            __syncthreads();
-            bb ^= 1;
+        compute(0, a, Bs + bb * BPL * XPLANE);
+        store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregA);
+        __syncthreads();
+        bb ^= 1;
+        // dy = 1
+        compute(1, a, Bs + bb * BPL * XPLANE);
+        store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregB);
+        __syncthreads();
+        bb ^= 1;
+        // dy = 2: fetch B of the next chunk's dy = 0; store it and the next halo (buffer idle since chunk cc-1)
+        if (morec) gload_b(g0 + 3, bregA);
+        compute(2, a, Bs + bb * BPL * XPLANE);
+        if (morec) {
+            store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregA);
+            store_halo(Hs + (hb ^ 1) * NS * HPLANE);
         }
+        __syncthreads();
+        bb ^= 1;
         hb ^= 1;
     }
+    unscale<NT>(acc, sx, op_scale<NT>(amax_w));
     ep(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
 }
 
@@ -768,7 +890,9 @@ static __device__ __forceinline__ int trswz(int row, int ch) {   // byte offset 
 template <int NT>
 __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float* __restrict__ dy, int lddy, int Cout,
                                                                      const float* __restrict__ x, int H, int W, int Cin,
-                                                                     int ldx, int K, int kt_per_split, EpiStore ep) {
+                                                                     int ldx, int K, int kt_per_split,
+                                                                     const float* amax_dy, const float* amax_x,
+                                                                     EpiStore ep) {
     constexpr int NS = XTerms<NT>::NS;
     constexpr int IMG = 16 * 128;                     // bf16 per [16 pix][128 ch] term image
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * NS * IMG];
@@ -789,6 +913,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
     const int ktiles = K / 16;
     const int kt0 = bz * kt_per_split;
     const int kt1 = min(ktiles, kt0 + kt_per_split);
+    const float sdy_ = op_scale<NT>(amax_dy), sx_ = op_scale<NT>(amax_x);
 
     f32x16 acc[2][2];
 #pragma unroll
@@ -827,7 +952,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
                 const float4 v = op ? rb[i] : ra[i];
                 const float xv[4] = {v.x, v.y, v.z, v.w};
                 __bf16 h[4], m[4], l[4];
-                split_terms<NS>(xv, h, m, l);
+                split_terms<NT>(xv, op ? sx_ : sdy_, h, m, l);
                 const int kk = kq + 8 * i;
                 char* d = reinterpret_cast<char*>(base + op * NS * IMG) + trswz(kk, c4 >> 3) + (c4 & 7) * 2;
                 *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
@@ -875,20 +1000,21 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
             for (int j = 0; j < 2; ++j) {
                 f32x16 c = acc[i][j];
                 if constexpr (NT >= 6) {
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+                    c = xmfma<NT>(fa[i][1], fb[j][1], c);
+                    c = xmfma<NT>(fa[i][2], fb[j][0], c);
+                    c = xmfma<NT>(fa[i][0], fb[j][2], c);
                 }
                 if constexpr (NT >= 3) {
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+                    c = xmfma<NT>(fa[i][1], fb[j][0], c);
+                    c = xmfma<NT>(fa[i][0], fb[j][1], c);
                 }
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+                acc[i][j] = xmfma<NT>(fa[i][0], fb[j][0], c);
             }
         if (more) sstore(smem + (cur ^ 1) * 2 * NS * IMG);
         __syncthreads();
         cur ^= 1;
     }
+    unscale<NT>(acc, sdy_, sx_);
     EpiStore e = ep;                       // this block's split slab (the epilogue would index blockIdx.z)
     e.y += (long long)bz * ep.zstride;
     e.zstride = 0;
@@ -897,16 +1023,18 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
 
 template <int WT>
 static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
-                            const EpiStoreW<4>& ep, int nterm, hipStream_t s) {
+                            const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm, hipStream_t s) {
     const int M = N * H * WT;
     dim3 grid(M / HBM_, (Cout + GBN - 1) / GBN, 1);
     switch (nterm) {
         case 1: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, ep); break;
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep); break;
         case 3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<3, WT, EpiStoreW<4>, true>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, ep); break;
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep); break;
+        case NT_H3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EpiStoreW<4>, true>), grid, dim3(HTHREADS), 0,
+                                       s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep); break;
         case 6: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<6, WT, EpiStoreW<4>, true>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, ep); break;
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep); break;
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();
@@ -927,6 +1055,56 @@ __global__ void split_bf16x3_kernel(const float* __restrict__ b, long long ldb, 
         const __bf16 l = (__bf16)(r1 - (float)m);
         __bf16* o = out + (((long long)kt * 3) * N + n) * XBK + kk;
         o[0] = h; o[(long long)N * XBK] = m; o[2LL * N * XBK] = l;
+    }
+}
+
+// b [K][N] fp32 (ld ldb) -> out [ceil(K/16)][3][N][16]: fp16 hi / lo of b * s (planes 0, 1), s = op_scale(max|b|)
+__global__ void split_f16x2_kernel(const float* __restrict__ b, long long ldb, int K, int N, const float* amax,
+                                   __bf16* __restrict__ out) {
+    const float sc = op_scale<NT_H3>(amax);
+    const int ktiles = (K + XBK - 1) / XBK;
+    const long long total = (long long)ktiles * N * XBK;
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long long)gridDim.x * blockDim.x) {
+        const int kk = (int)(q % XBK); const long long r = q / XBK;
+        const int n = (int)(r % N); const int kt = (int)(r / N);
+        const int k = kt * XBK + kk;
+        const float v = (k < K ? b[(long long)k * ldb + n] : 0.f) * sc;
+        const _Float16 h = (_Float16)v;
+        __bf16* o = out + (((long long)kt * 3) * N + n) * XBK + kk;
+        o[0] = __builtin_bit_cast(__bf16, h);
+        o[(long long)N * XBK] = __builtin_bit_cast(__bf16, (_Float16)(v - (float)h));
+    }
+}
+
+// out = max(out, max |x[r*ld + c]|) over r < rows, c < C  (atomic max on the float's bits; NaN ignored)
+__global__ void amax_kernel(const float* __restrict__ x, long long rows, int C, long long ld, unsigned* out) {
+    float m = 0.f;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (C % 4 == 0 && ld % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+        const int C4 = C / 4;
+        const long long total = rows * C4;
+        for (long long q = t0; q < total; q += stride) {
+            const long long r = q / C4; const int c = (int)(q - r * C4) * 4;
+            const float4 v = *reinterpret_cast<const float4*>(x + r * ld + c);
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        }
+    } else {
+        const long long total = rows * C;
+        for (long long q = t0; q < total; q += stride) {
+            const long long r = q / C; const int c = (int)(q - r * C);
+            m = fmaxf(m, fabsf(x[r * ld + c]));
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    __shared__ float wm[8];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) wm[w] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, wm[i]);
+        atomicMax(out, __float_as_uint(m));
     }
 }
 
@@ -1006,40 +1184,56 @@ CDM_API int cdm_conv3x3_fwd_variant(int variant, const float* x, int N, int H, i
     }
 }
 
-// fp32-accurate conv3x3 forward on the bf16 matrix cores (split terms, see gemm_x3_kernel).
-// wx3 = cdm_split_bf16x3 of the fp32 packed weights (same K order kc as cdm_pack_conv3x3).
-CDM_API int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx3,
-                               const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
-                               int kc, int nterm, void* stream) {
+// conv3x3 forward on the 16-bit matrix cores in arithmetic nterm (split terms, see gemm_x3_kernel);
+// wx = the split packed weights (cdm_split_bf16x3 / cdm_split_f16x2, same K order kc as cdm_pack_conv3x3).
+static int conv3x3_fwd_split(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
+                             const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags,
+                             float* stats, int stats_ld, int kc, int nterm, float* amax_y, hipStream_t st) {
     if (Cin % 4 || Cout % 4 || (kc != 0 && kc != 16) || (kc == 16 && Cin % 16)) return (int)hipErrorInvalidValue;
     const int M = N * H * W, K = 9 * Cin;
-    MkPre mb{reinterpret_cast<const __bf16*>(wx3), Cout};
-    EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout};
-    hipStream_t st = S(stream);
+    MkPre mb{reinterpret_cast<const __bf16*>(wx), Cout, amax_w};
+    EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
     if (kc == 16 && W == H && (W == 64 || W == 32) && ldx % 4 == 0 && (H * W) % HBM_ == 0) {   // LDS-halo path
-        const EpiStoreW<4> eh{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout};
-        const __bf16* b = reinterpret_cast<const __bf16*>(wx3);
-        return W == 64 ? launch_conv_halo<64>(x, N, H, Cin, ldx, b, Cout, eh, nterm, st)
-                       : launch_conv_halo<32>(x, N, H, Cin, ldx, b, Cout, eh, nterm, st);
+        const EpiStoreW<4> eh{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
+        const __bf16* b = reinterpret_cast<const __bf16*>(wx);
+        return W == 64 ? launch_conv_halo<64>(x, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st)
+                       : launch_conv_halo<32>(x, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st);
     }
     if (Cin == 128 && Cout == 128 && H == 64 && W == 64 && kc == 16) {
         using LA = LdIm2colA<128, 16, 64>;
-        return launch_gemm_x3<RowK<LA>::template T, StagePre, EpiStore, true>(MkRowK<LA>{LA{x, H, W, Cin, ldx, M, K}}, mb,
-                                                                             ep, M, Cout, K, 1, nterm, st);
+        return launch_gemm_x3<RowK<LA>::template T, StagePre, EpiStore, true>(
+            MkRowK<LA>{LA{x, H, W, Cin, ldx, M, K}, amax_x}, mb, ep, M, Cout, K, 1, nterm, st);
     }
     if (kc == 16) {
         using LA = LdIm2colA<0, 16>;
-        return launch_gemm_x3<RowK<LA>::template T, StagePre, EpiStore, true>(MkRowK<LA>{LA{x, H, W, Cin, ldx, M, K}}, mb,
-                                                                             ep, M, Cout, K, 1, nterm, st);
+        return launch_gemm_x3<RowK<LA>::template T, StagePre, EpiStore, true>(
+            MkRowK<LA>{LA{x, H, W, Cin, ldx, M, K}, amax_x}, mb, ep, M, Cout, K, 1, nterm, st);
     }
     using LA = LdIm2colA<0, 0>;
-    return launch_gemm_x3<RowK<LA>::template T, StagePre, EpiStore, true>(MkRowK<LA>{LA{x, H, W, Cin, ldx, M, K}}, mb, ep,
-                                                                         M, Cout, K, 1, nterm, st);
+    return launch_gemm_x3<RowK<LA>::template T, StagePre, EpiStore, true>(
+        MkRowK<LA>{LA{x, H, W, Cin, ldx, M, K}, amax_x}, mb, ep, M, Cout, K, 1, nterm, st);
 }
 
-// conv3x3 weight gradient on the split-bf16 path (same slab contract as cdm_conv3x3_wgrad); W % 8 == 0
-CDM_API int cdm_conv3x3_wgrad_x3(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,
-                                 int ldx, int splits, float* slab, int nterm, void* stream) {
+CDM_API int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx3,
+                               const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
+                               int kc, int nterm, void* stream) {
+    if (nterm != 1 && nterm != 3 && nterm != 6) return (int)hipErrorInvalidValue;
+    return conv3x3_fwd_split(x, N, H, W, Cin, ldx, wx3, nullptr, nullptr, bias, y, ldy, Cout, flags, stats, stats_ld, kc,
+                             nterm, nullptr, S(stream));
+}
+
+CDM_API int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
+                               const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags,
+                               float* stats, int stats_ld, int kc, float* amax_y, void* stream) {
+    if (!amax_x || !amax_w) return (int)hipErrorInvalidValue;
+    return conv3x3_fwd_split(x, N, H, W, Cin, ldx, wx, amax_x, amax_w, bias, y, ldy, Cout, flags, stats, stats_ld, kc,
+                             NT_H3, amax_y, S(stream));
+}
+
+// conv3x3 weight gradient on the 16-bit matrix cores (same slab contract as cdm_conv3x3_wgrad); W % 8 == 0
+static int conv3x3_wgrad_split(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,
+                               int ldx, const float* amax_dy, const float* amax_x, int splits, float* slab, int nterm,
+                               hipStream_t st) {
     if (Cin % 4 || Cout % 4 || W % 8) return (int)hipErrorInvalidValue;
     const int M = Cout, NN = 9 * Cin, K = N * H * W;
     const int sp = effective_splits(K, splits);
@@ -1048,40 +1242,83 @@ CDM_API int cdm_conv3x3_wgrad_x3(const float* dy, int lddy, int Cout, const floa
         effective_splits(K, splits, 16) == sp) {   // transposed-read path
         const int ktiles = K / 16, per = (ktiles + sp - 1) / sp;
         dim3 grid((M / GBM) * (NN / GBN) * ((ktiles + per - 1) / per));
-        hipStream_t st = S(stream);
         switch (nterm) {
             case 1: hipLaunchKernelGGL(wgrad3x3_tr_x3_kernel<1>, grid, dim3(GTHREADS), 0, st, dy, lddy, Cout, x, H, W, Cin,
-                                       ldx, K, per, ep); break;
+                                       ldx, K, per, amax_dy, amax_x, ep); break;
             case 3: hipLaunchKernelGGL(wgrad3x3_tr_x3_kernel<3>, grid, dim3(GTHREADS), 0, st, dy, lddy, Cout, x, H, W, Cin,
-                                       ldx, K, per, ep); break;
+                                       ldx, K, per, amax_dy, amax_x, ep); break;
+            case NT_H3: hipLaunchKernelGGL(wgrad3x3_tr_x3_kernel<NT_H3>, grid, dim3(GTHREADS), 0, st, dy, lddy, Cout, x, H,
+                                           W, Cin, ldx, K, per, amax_dy, amax_x, ep); break;
             case 6: hipLaunchKernelGGL(wgrad3x3_tr_x3_kernel<6>, grid, dim3(GTHREADS), 0, st, dy, lddy, Cout, x, H, W, Cin,
-                                       ldx, K, per, ep); break;
+                                       ldx, K, per, amax_dy, amax_x, ep); break;
             default: return (int)hipErrorInvalidValue;
         }
         return cdm_status();
     }
     return launch_gemm_x3<ColK<LdDenseAT>::template T, ColK<LdIm2colB>::template T, EpiStore, false>(
-        MkColK<LdDenseAT>{LdDenseAT{dy, lddy, M, K}}, MkColK<LdIm2colB>{LdIm2colB{x, H, W, Cin, ldx, K, NN}}, ep, M, NN,
-        K, sp, nterm, S(stream));
+        MkColK<LdDenseAT>{LdDenseAT{dy, lddy, M, K}, amax_dy}, MkColK<LdIm2colB>{LdIm2colB{x, H, W, Cin, ldx, K, NN}, amax_x},
+        ep, M, NN, K, sp, nterm, st);
+}
+
+CDM_API int cdm_conv3x3_wgrad_x3(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,
+                                 int ldx, int splits, float* slab, int nterm, void* stream) {
+    if (nterm != 1 && nterm != 3 && nterm != 6) return (int)hipErrorInvalidValue;
+    return conv3x3_wgrad_split(dy, lddy, Cout, x, N, H, W, Cin, ldx, nullptr, nullptr, splits, slab, nterm, S(stream));
+}
+
+CDM_API int cdm_conv3x3_wgrad_h3(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,
+                                 int ldx, const float* amax_dy, const float* amax_x, int splits, float* slab,
+                                 void* stream) {
+    if (!amax_dy || !amax_x) return (int)hipErrorInvalidValue;
+    return conv3x3_wgrad_split(dy, lddy, Cout, x, N, H, W, Cin, ldx, amax_dy, amax_x, splits, slab, NT_H3, S(stream));
+}
+
+static int split_blocks(int K, int N) {
+    const long long total = (long long)((K + XBK - 1) / XBK) * N * XBK;
+    long long blocks = (total + 255) / 256;
+    return (int)(blocks > 8192 ? 8192 : (blocks < 1 ? 1 : blocks));
 }
 
 CDM_API int cdm_split_bf16x3(const float* b, long long ldb, int K, int N, void* out, void* stream) {
-    const long long total = (long long)((K + XBK - 1) / XBK) * N * XBK;
-    int blocks = (int)((total + 255) / 256);
-    if (blocks > 8192) blocks = 8192;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(split_bf16x3_kernel, dim3(blocks), dim3(256), 0, S(stream), b, ldb, K, N,
+    hipLaunchKernelGGL(split_bf16x3_kernel, dim3(split_blocks(K, N)), dim3(256), 0, S(stream), b, ldb, K, N,
                        reinterpret_cast<__bf16*>(out));
     return cdm_status();
 }
 
+CDM_API int cdm_split_f16x2(const float* b, long long ldb, int K, int N, const float* amax, void* out, void* stream) {
+    if (!amax) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(split_f16x2_kernel, dim3(split_blocks(K, N)), dim3(256), 0, S(stream), b, ldb, K, N, amax,
+                       reinterpret_cast<__bf16*>(out));
+    return cdm_status();
+}
+
+CDM_API int cdm_zero_f32(float* p, long long n, void* stream) {
+    return n > 0 ? (int)hipMemsetAsync(p, 0, (size_t)n * sizeof(float), S(stream)) : 0;
+}
+
+CDM_API int cdm_amax_f32(const float* x, long long rows, int C, long long ld, float* out, int accumulate,
+                         void* stream) {
+    if (rows < 0 || C < 0 || ld < C) return (int)hipErrorInvalidValue;
+    if (!accumulate) {
+        const hipError_t e = hipMemsetAsync(out, 0, sizeof(float), S(stream));
+        if (e != hipSuccess) return (int)e;
+    }
+    const long long total = rows * (long long)C;
+    if (total == 0) return 0;
+    long long blocks = (total / 4 + 255) / 256;
+    blocks = blocks > 2048 ? 2048 : (blocks < 1 ? 1 : blocks);
+    hipLaunchKernelGGL(amax_kernel, dim3((int)blocks), dim3(256), 0, S(stream), x, rows, C, ld,
+                       reinterpret_cast<unsigned*>(out));
+    return cdm_status();
+}
+
 CDM_API int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk,
-                             const float* bias, float* y, int ldy, int Cout, void* stream) {
+                             const float* bias, float* y, int ldy, int Cout, float* amax, void* stream) {
     if (Cin % 4 || Cout % 4) return (int)hipErrorInvalidValue;
     const int M = N * H * W, K = Cin, NN = 4 * Cout;
     LdDenseA la{x, ldx, M, K};
     LdDenseB lb{wpk, NN, K, NN};
-    EpiConvT2x2 ep{y, ldy, bias, H, W, Cout, M, NN};
+    EpiConvT2x2 ep{y, ldy, bias, H, W, Cout, M, NN, amax};
     return launch_gemm<LdDenseA, LdDenseB, EpiConvT2x2, false>(la, lb, ep, M, NN, K, 1, S(stream));
 }
 

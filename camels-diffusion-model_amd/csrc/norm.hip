@@ -310,8 +310,10 @@ __global__ void col_sum_kernel(const float* in, int N, int C, float* out, int ac
 // -------------------------------------------------------------------------------------------------
 template <bool POOL, bool FILM, bool RESID, bool RELU>
 __global__ __launch_bounds__(256) void norm_apply_fwd_kernel(const float* y, int ldy, int N, int H, int W, int C,
-                                                             NormP np, FilmP fp, ResidP rp, float* out, int ldo) {
+                                                             NormP np, FilmP fp, ResidP rp, float* out, int ldo,
+                                                             float* amax) {
     const int C4 = C >> 2;
+    float am = 0.f;
     const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
     const long long total = (long long)N * Ho * Wo * C4;
     for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -351,7 +353,9 @@ __global__ __launch_bounds__(256) void norm_apply_fwd_kernel(const float* y, int
             }
         }
         st4(out + pix * ldo + c4, make_float4(o[0], o[1], o[2], o[3]));
+        am = fmaxf(am, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
     }
+    if (amax) block_amax_commit(am, amax);
 }
 
 // elementwise backward apply: dy = A*g_pre + B + Cc*xhat   (full grid; pooled / FiLM'd g_out recomputed)
@@ -359,8 +363,9 @@ template <bool POOL, bool FILM>
 __global__ __launch_bounds__(256) void norm_apply_bwd_kernel(const float* g, int ldg, const float* y, int ldy, int N,
                                                              int H, int W, int C, NormP np, FilmP fp, const float* A,
                                                              const float* B, const float* Cc, int cn, float* dy,
-                                                             int lddy) {
+                                                             int lddy, float* amax) {
     const int C4 = C >> 2;
+    float am = 0.f;
     const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
     const long long total = (long long)N * Ho * Wo * C4;
     for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -395,9 +400,12 @@ __global__ __launch_bounds__(256) void norm_apply_bwd_kernel(const float* g, int
                 }
             }
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
+            for (int e = 0; e < 4; ++e) {
                 st4(dy + ((long long)(n * H + 2 * ho + (e >> 1)) * W + 2 * wo + (e & 1)) * lddy + c4,
                     make_float4(out[e][0], out[e][1], out[e][2], out[e][3]));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) am = fmaxf(am, fabsf(out[e][j]));
+            }
         } else {
             const float4 yv = ld4(y + pix * ldy + c4);
             float out[4];
@@ -411,8 +419,11 @@ __global__ __launch_bounds__(256) void norm_apply_bwd_kernel(const float* g, int
                 out[j] = A[n * cn + c] * gpre + B[n * cn + c] + Cc[n * cn + c] * xh;
             }
             st4(dy + pix * lddy + c4, make_float4(out[0], out[1], out[2], out[3]));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) am = fmaxf(am, fabsf(out[j]));
         }
     }
+    if (amax) block_amax_commit(am, amax);
 }
 
 static inline int ew_blocks(long long total) {
@@ -514,7 +525,7 @@ CDM_API int cdm_col_sum(const float* in, int N, int C, float* out, int accumulat
 CDM_API int cdm_norm_apply_fwd(int flags, const float* y, int ldy, int N, int H, int W, int C, const float* s,
                                const float* t, int sn, const float* film_a, int film_an, const float* film_b,
                                int film_bn, const float* rx, const float* rw, const float* rb, int rsplit, float* out,
-                               int ldo, void* stream) {
+                               int ldo, float* amax, void* stream) {
     if (C % 4) return (int)hipErrorInvalidValue;
     NormP np{s, t, sn, nullptr, nullptr, 0, 1};
     FilmP fp{film_a, film_an, film_b, film_bn};
@@ -523,7 +534,7 @@ CDM_API int cdm_norm_apply_fwd(int flags, const float* y, int ldy, int N, int H,
     const long long total = (long long)N * (pool ? (H / 2) * (W / 2) : H * W) * (C / 4);
     const int nb = ew_blocks(total);
 #define CDM_APPLY(P, F, Rz, Rl) \
-    hipLaunchKernelGGL((norm_apply_fwd_kernel<P, F, Rz, Rl>), dim3(nb), dim3(256), 0, S(stream), y, ldy, N, H, W, C, np, fp, rp, out, ldo)
+    hipLaunchKernelGGL((norm_apply_fwd_kernel<P, F, Rz, Rl>), dim3(nb), dim3(256), 0, S(stream), y, ldy, N, H, W, C, np, fp, rp, out, ldo, amax)
     if (pool) {
         if (film || resid) return (int)hipErrorInvalidValue;
         if (relu) CDM_APPLY(true, false, false, true); else CDM_APPLY(true, false, false, false);
@@ -542,7 +553,7 @@ CDM_API int cdm_norm_apply_fwd(int flags, const float* y, int ldy, int N, int H,
 CDM_API int cdm_norm_apply_bwd(int mode, const float* g, int ldg, const float* y, int ldy, int N, int H, int W, int C,
                                const float* s, const float* t, int sn, const float* mean, const float* invstd, int mn,
                                int cpg, const float* film_a, int film_an, const float* A, const float* B,
-                               const float* Cc, int cn, float* dy, int lddy, void* stream) {
+                               const float* Cc, int cn, float* dy, int lddy, float* amax, void* stream) {
     if (C % 4) return (int)hipErrorInvalidValue;
     NormP np{s, t, sn, mean, invstd, mn, cpg};
     FilmP fp{film_a, film_an, nullptr, 0};
@@ -550,12 +561,12 @@ CDM_API int cdm_norm_apply_bwd(int mode, const float* g, int ldg, const float* y
     const int nb = ew_blocks(total);
     if (mode == 1)
         hipLaunchKernelGGL((norm_apply_bwd_kernel<true, false>), dim3(nb), dim3(256), 0, S(stream), g, ldg, y, ldy, N, H, W,
-                           C, np, fp, A, B, Cc, cn, dy, lddy);
+                           C, np, fp, A, B, Cc, cn, dy, lddy, amax);
     else if (mode == 2)
         hipLaunchKernelGGL((norm_apply_bwd_kernel<false, true>), dim3(nb), dim3(256), 0, S(stream), g, ldg, y, ldy, N, H,
-                           W, C, np, fp, A, B, Cc, cn, dy, lddy);
+                           W, C, np, fp, A, B, Cc, cn, dy, lddy, amax);
     else
         hipLaunchKernelGGL((norm_apply_bwd_kernel<false, false>), dim3(nb), dim3(256), 0, S(stream), g, ldg, y, ldy, N, H,
-                           W, C, np, fp, A, B, Cc, cn, dy, lddy);
+                           W, C, np, fp, A, B, Cc, cn, dy, lddy, amax);
     return cdm_status();
 }

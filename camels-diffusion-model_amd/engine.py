@@ -93,9 +93,12 @@ def conv_layers(nf: int, H: int):
 
 
 # 3x3 conv arithmetic: "fp32" = fp32 MFMA (v_mfma_f32_32x32x2_f32); "x6" = fp32-accurate split-bf16
-# (6 cross terms on v_mfma_f32_32x32x16_bf16, see csrc/gemm_f32.hip); "x3" / "bf16" = reduced-precision
-# variants (bf16x3 / plain bf16 operands, fp32 accumulate) for the mixed-precision configuration.
-CONV_MATH = {"fp32": 0, "x6": 6, "x3": 3, "bf16": 1}
+# (6 cross terms on v_mfma_f32_32x32x16_bf16, see csrc/gemm_f32.hip); "h3" = fp32-class scaled fp16
+# hi/lo split (3 cross terms on v_mfma_f32_32x32x16_f16; per-tensor power-of-two scale from max|.|);
+# "x3" / "bf16" = reduced-precision variants (bf16x3 / plain bf16 operands, fp32 accumulate) for the
+# mixed-precision configuration.
+CONV_MATH = {"fp32": 0, "x6": 6, "x3": 3, "bf16": 1, "h3": 4}
+NT_H3 = 4
 
 MLPS = ("contextembed1", "timeembed1", "contextembed2", "timeembed2")
 
@@ -120,6 +123,7 @@ class UNetEngine:
         self._pk_key = None
         self._ones = torch.ones(4 * n_feat, device=self.device)
         self._zeros = torch.zeros(4 * n_feat, device=self.device)
+        self._amax = torch.zeros(2, device=self.device)     # h3: max|A|, max|B| of the current launch
 
     # ------------------------------------------------------------------------------------------
     # weight packing (OIHW / [Cin][Cout][kh][kw] -> GEMM layouts; eval: BatchNorm folded)
@@ -190,21 +194,63 @@ class UNetEngine:
         return t
 
     def _split(self, name, K, N, stream):
-        """bf16 hi/mid/lo split of the packed fp32 [K][N] weights pk[name] -> pk[name + "_x"]."""
+        """16-bit split of the packed fp32 [K][N] weights pk[name] -> pk[name + "_x"] (bf16 hi/mid/lo, or
+        for h3 the scaled fp16 hi/lo with max|W| in pk[name + "_amax"])."""
         if not self.nterm:
             return
         xb = self._buf(name + "_x", (_cdiv(K, 16) * 3 * N * 16,), torch.bfloat16)
-        lib().cdm_split_bf16x3(_p(self.pk[name]), N, K, N, _p(xb), stream)
+        if self.nterm == NT_H3:
+            am = self._buf(name + "_amax", (1,))
+            lib().cdm_amax_f32(_p(self.pk[name]), K, N, N, _p(am), 0, stream)
+            lib().cdm_split_f16x2(_p(self.pk[name]), N, K, N, _p(am), _p(xb), stream)
+            self.pk[name + "_amax"] = am
+        else:
+            lib().cdm_split_bf16x3(_p(self.pk[name]), N, K, N, _p(xb), stream)
         self.pk[name + "_x"] = xb
 
-    def conv3x3(self, key, x_p, B, S, cin, ldx, bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, s):
-        """3x3 conv (fwd or dgrad) with the packed weights pk[key], in this engine's conv arithmetic."""
-        if self.nterm:
+    def conv3x3(self, key, x_p, B, S, cin, ldx, bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, s,
+                amax_x=None, amax_y=None):
+        """3x3 conv (fwd or dgrad) with the packed weights pk[key], in this engine's conv arithmetic.
+
+        h3 only: amax_x = device max|x| written by x's producer (None: measured here by a separate pass);
+        amax_y = slot that receives max|y| for the next conv."""
+        if self.nterm == NT_H3:
+            if amax_x is None:
+                amax_x = _p(self._amax)
+                lib().cdm_amax_f32(x_p, B * S * S, cin, ldx, amax_x, 0, s)
+            lib().cdm_conv3x3_fwd_h3(x_p, B, S, S, cin, ldx, _p(self.pk[key + "_x"]), amax_x,
+                                     _p(self.pk[key + "_amax"]), bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc,
+                                     amax_y, s)
+        elif self.nterm:
             lib().cdm_conv3x3_fwd_x3(x_p, B, S, S, cin, ldx, _p(self.pk[key + "_x"]), bias_p, y_p, ldy, cout, flags,
                                      stats_p, stats_ld, kc, self.nterm, s)
         else:
             lib().cdm_conv3x3_fwd(x_p, B, S, S, cin, ldx, _p(self.pk[key]), bias_p, y_p, ldy, cout, flags, stats_p,
                                   stats_ld, kc, s)
+
+    # h3 operand maxima: one device slot per producer, zeroed at the start of every forward --------------
+    def _slot(self, ws, key):
+        """Pointer to the amax slot `key` of this workspace (None unless the arithmetic is h3)."""
+        if self.nterm != NT_H3:
+            return None
+        i = ws.aslot.get(key)
+        if i is None:
+            i = ws.aslot[key] = len(ws.aslot)
+            assert i < ws.amax.numel()
+        return _p(ws.amax) + 4 * i
+
+    def _dst_slot(self, ws, l: "LayerSpec"):
+        # catO's two producers (init_conv output x0, up2 output) share one slot: out.0 reads both halves
+        return self._slot(ws, "catO" if l.name in ("init_conv.conv2", "up2.model.2.conv2") else "z:" + l.name)
+
+    def _src_slot(self, ws, l: "LayerSpec"):
+        special = {"down1.model.0.conv1": "catO", "down2.model.0.conv1": "z:down1.model.1.conv2",
+                   "up1.model.1.conv1": "yT1", "up2.model.1.conv1": "yT2"}
+        if l.name in special:
+            return self._slot(ws, special[l.name])
+        i = self.layers.index(l)
+        return self._slot(ws, "catO" if self.layers[i - 1].name in ("init_conv.conv2",) else
+                          "z:" + self.layers[i - 1].name)
 
     # ------------------------------------------------------------------------------------------
     def workspace(self, B: int, train: bool) -> "Workspace":
@@ -226,6 +272,8 @@ class UNetEngine:
         eps = out if out is not None else ws.eps
         ws.x_in = x
         ws.sc_pending = (sc_w, sc_b, sc_split)
+        if self.nterm == NT_H3:
+            lb.cdm_zero_f32(_p(ws.amax), ws.amax.numel(), s)
         # ---------------- encoder ----------------
         for l in self.layers[:10]:
             self._conv_bn_fwd(ws, P, l, s, x)
@@ -263,23 +311,23 @@ class UNetEngine:
         u1 = ws.catU1.sl(0, c0)
         lb.cdm_norm_apply_fwd(APPLY_FILM | APPLY_RELU, _p(ws.y0), c0, B, H2, H2, c0, _p(ws.gn0["scale"]),
                               _p(ws.gn0["shift"]), c0, _p(ce1), c0 if rows_c > 1 else 0, _p(te1),
-                              c0 if rows_t > 1 else 0, None, None, None, 0, u1.p, u1.ld, s)
+                              c0 if rows_t > 1 else 0, None, None, None, 0, u1.p, u1.ld, None, s)
         # ---------------- up1 ----------------
         lb.cdm_convT2x2_fwd(ws.catU1.p, B, H2, H2, 4 * nf, 4 * nf, _p(self.pk["up1.model.0.wt"]),
-                            _p(P["up1.model.0.bias"]), _p(ws.yT1), nf, nf, s)
+                            _p(P["up1.model.0.bias"]), _p(ws.yT1), nf, nf, self._slot(ws, "yT1"), s)
         for l in self.layers[10:14]:
             self._conv_bn_fwd(ws, P, l, s, x)
         # ---------------- up2 ----------------
         lb.cdm_convT2x2_fwd(ws.catU2.p, B, H1, H1, 2 * nf, 2 * nf, _p(self.pk["up2.model.0.wt"]),
-                            _p(P["up2.model.0.bias"]), _p(ws.yT2), nf, nf, s)
+                            _p(P["up2.model.0.bias"]), _p(ws.yT2), nf, nf, self._slot(ws, "yT2"), s)
         for l in self.layers[14:18]:
             self._conv_bn_fwd(ws, P, l, s, x)
         # ---------------- out ----------------
         self.conv3x3("out.0.wpk", ws.catO.p, B, H, 2 * nf, 2 * nf, _p(P["out.0.bias"]), _p(ws.yO), nf, nf, 0,
-                     _p(ws.slab), nf, self.kc_out0, s)
+                     _p(ws.slab), nf, self.kc_out0, s, amax_x=self._slot(ws, "catO"))
         self._gn_fwd(ws, P, "out.1", Act(ws.yO, nf), B, H, nf, ws.gnO, stats_from_conv=True, stream=s)
         lb.cdm_norm_apply_fwd(APPLY_RELU, _p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]), _p(ws.gnO["shift"]), nf,
-                              None, 0, None, 0, None, None, None, 0, _p(ws.zO), nf, s)
+                              None, 0, None, 0, None, None, None, 0, _p(ws.zO), nf, None, s)
         lb.cdm_conv3x3_cout1_fwd(_p(ws.zO), nf, B, H, H, nf, _p(P["out.3.weight"]), _p(P["out.3.bias"]), _p(eps), s)
         return eps
 
@@ -298,7 +346,7 @@ class UNetEngine:
                 ntiles = B * _cdiv(S * S, CHUNK)
             else:
                 self.conv3x3(l.name + ".wpk", src.p, B, S, l.cin, src.ld, _p(P[l.b]), _p(y), l.cout, l.cout, 0,
-                             _p(ws.slab), l.cout, l.kc, s)
+                             _p(ws.slab), l.cout, l.kc, s, amax_x=self._src_slot(ws, l))
                 ntiles = _cdiv(npix, CHUNK)
             bn = l.bn
             nparts = fold(ws, _p(ws.slab), ntiles, 2, l.cout, s)
@@ -311,12 +359,16 @@ class UNetEngine:
             kind = ws.dst_kind[l.name]
             dense = kind in ("dense", "plain")
             outp = ws.dst[l.name] if dense else Act(y, l.cout)
+            dslot = self._dst_slot(ws, l) if dense else None
             if l.cin == 1:
                 lb.cdm_conv3x3_cin1_fwd(_p(x), B, S, S, _p(self.pk[l.name + ".wpk_e"]),
                                         _p(self.pk[l.name + ".bpk_e"]), outp.p, outp.ld, l.cout, 1, s)
+                if dslot is not None:   # the direct C_in = 1 conv has no fused max: one pass over its output
+                    lb.cdm_amax_f32(outp.p, B * S * S, l.cout, outp.ld, dslot, 1, s)
             else:
                 self.conv3x3(l.name + ".wpk_e", src.p, B, S, l.cin, src.ld, _p(self.pk[l.name + ".bpk_e"]), outp.p,
-                             outp.ld, l.cout, EPI_RELU, None, 0, l.kc, s)
+                             outp.ld, l.cout, EPI_RELU, None, 0, l.kc, s, amax_x=self._src_slot(ws, l),
+                             amax_y=dslot)
             if dense:
                 return
             scale, shift, relu = self._ones, self._zeros, 0
@@ -324,21 +376,22 @@ class UNetEngine:
         kind = ws.dst_kind[l.name]
         dst = ws.dst[l.name]
         C = l.cout
+        am = self._dst_slot(ws, l) if kind != "film" else None    # FiLM2 output feeds the fp32 ConvT
         if kind == "dense" or kind == "plain":
             lb.cdm_norm_apply_fwd(relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), 0, None, 0, None, 0, None, None,
-                                  None, 0, dst.p, dst.ld, s)
+                                  None, 0, dst.p, dst.ld, am, s)
         elif kind == "pool":
             lb.cdm_norm_apply_fwd(APPLY_POOL | relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), 0, None, 0, None, 0,
-                                  None, None, None, 0, dst.p, dst.ld, s)
+                                  None, None, None, 0, dst.p, dst.ld, am, s)
         elif kind == "film":
             ce, te = ws.emb["contextembed2"], ws.emb["timeembed2"]
             lb.cdm_norm_apply_fwd(APPLY_FILM | relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), 0, _p(ce),
                                   C if ws.c_rows > 1 else 0, _p(te), C if ws.t_rows > 1 else 0, None, None, None, 0,
-                                  dst.p, dst.ld, s)
+                                  dst.p, dst.ld, am, s)
         elif kind == "resid":
             sc_w, sc_b, split = ws.sc_pending
             lb.cdm_norm_apply_fwd(APPLY_RESID | relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), 0, None, 0, None,
-                                  0, _p(x), _p(sc_w), _p(sc_b), split, dst.p, dst.ld, s)
+                                  0, _p(x), _p(sc_w), _p(sc_b), split, dst.p, dst.ld, am, s)
         else:
             raise AssertionError(kind)
 
@@ -379,12 +432,14 @@ class UNetEngine:
         lb.cdm_conv3x3_cout1_dgrad(_p(deps), B, H, H, nf, _p(P["out.3.weight"]), _p(gO), nf, s)
         # ---------------- out.1 GroupNorm + ReLU ----------------
         dyO = ws.D0
+        dslot = self._slot(ws, "dy:out.0")
         self._gn_bwd(ws, P, "out.1", "out.0.bias", Act(gO, nf), 0, Act(ws.yO, nf), B, H, nf, ws.gnO, None, 0,
-                     Act(dyO, nf), G, s)
+                     Act(dyO, nf), G, s, amax=dslot)
         # ---------------- out.0 conv (2nf -> nf) ----------------
-        self._wgrad3x3(ws, Act(dyO, nf), ws.catO, B, H, 2 * nf, nf, G["out.0.weight"], s)
+        self._wgrad3x3(ws, Act(dyO, nf), ws.catO, B, H, 2 * nf, nf, G["out.0.weight"], s, amax_dy=dslot,
+                       amax_x=self._slot(ws, "catO"))
         self.conv3x3("out.0.wdg", _p(dyO), B, H, nf, nf, None, ws.dcatO.p, ws.dcatO.ld, 2 * nf, 0, None, 0,
-                     self.kc_out0, s)
+                     self.kc_out0, s, amax_x=dslot)
         hook("out")
         # ---------------- up2 blocks ----------------
         self._chain_bwd(ws, P, self.layers[14:18], G, s)
@@ -462,24 +517,34 @@ class UNetEngine:
                                _p(G[bn + ".weight"]), _p(G[bn + ".bias"]), _p(co[0]), _p(co[1]), _p(co[2]),
                                _p(G[l.b]), s)
         dy = ws.dy[l.name]
+        dslot = self._slot(ws, "dy:" + l.name) if l.cin > 1 else None
         lb.cdm_norm_apply_bwd(mode, g.p, g.ld, _p(y), C, B, S, S, C, _p(st["scale"]), _p(st["shift"]), 0,
                               _p(st["mean"]), _p(st["invstd"]), 0, 1, _p(film_a), film_an, _p(co[0]), _p(co[1]),
-                              _p(co[2]), 0, dy.p, dy.ld, s)
+                              _p(co[2]), 0, dy.p, dy.ld, dslot, s)
         src = ws.src[l.name]
         if l.cin == 1:
             lb.cdm_conv3x3_cin1_wgrad(dy.p, dy.ld, _p(ws.x_in), B, S, S, C, CHUNK, _p(ws.slab), s)
             nparts = fold(ws, _p(ws.slab), B * _cdiv(S * S, CHUNK), 10, C, s)
             lb.cdm_slab_sum_all(_p(ws.dpart), nparts, 10, 0, 9, C, _p(G[l.w]), 1, 9, 0, s)
             return
-        self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s)
+        self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s, amax_dy=dslot, amax_x=self._src_slot(ws, l))
         dgd = ws.dgrad_dst[l.name]
         self.conv3x3(l.name + ".wdg", dy.p, B, S, C, dy.ld, None, dgd.p, dgd.ld, l.cin,
-                     EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s)
+                     EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s, amax_x=dslot)
 
-    def _wgrad3x3(self, ws, dy: Act, x: Act, B, S, cin, cout, gW, s):
+    def _wgrad3x3(self, ws, dy: Act, x: Act, B, S, cin, cout, gW, s, amax_dy=None, amax_x=None):
         lb = lib()
         sp = wgrad_splits(B * S * S, cout, 9 * cin)
-        if self.nterm:
+        if self.nterm == NT_H3:
+            am = _p(self._amax)
+            if amax_dy is None:
+                amax_dy = am
+                lb.cdm_amax_f32(dy.p, B * S * S, cout, dy.ld, amax_dy, 0, s)
+            if amax_x is None:
+                amax_x = am + 4
+                lb.cdm_amax_f32(x.p, B * S * S, cin, x.ld, amax_x, 0, s)
+            lb.cdm_conv3x3_wgrad_h3(dy.p, dy.ld, cout, x.p, B, S, S, cin, x.ld, amax_dy, amax_x, sp, _p(ws.slab), s)
+        elif self.nterm:
             lb.cdm_conv3x3_wgrad_x3(dy.p, dy.ld, cout, x.p, B, S, S, cin, x.ld, sp, _p(ws.slab), self.nterm, s)
         else:
             lb.cdm_conv3x3_wgrad(dy.p, dy.ld, cout, x.p, B, S, S, cin, x.ld, sp, _p(ws.slab), s)
@@ -500,7 +565,7 @@ class UNetEngine:
         lb.cdm_convT2x2_dgrad(gy.p, B, Hin, Hin, cout, gy.ld, _p(self.pk[name + ".wtT"]), dx.p, dx.ld, cin, 0, s)
 
     def _gn_bwd(self, ws, P, name, bias_name, g: Act, mode, y: Act, B, S, C, st, film_a, film_an, dy: Act, G, s,
-                film_out=None):
+                film_out=None, amax=None):
         lb = lib()
         nch = _cdiv(S * S, CHUNK)
         cpg = C // GN_GROUPS
@@ -519,7 +584,7 @@ class UNetEngine:
             lb.cdm_col_sum(_p(co[5]), B, C, _p(G[bias_name]), 0, s)
         lb.cdm_norm_apply_bwd(mode, g.p, g.ld, y.p, y.ld, B, S, S, C, _p(st["scale"]), _p(st["shift"]), C,
                               _p(st["mean"]), _p(st["invstd"]), GN_GROUPS, cpg, _p(film_a), film_an, _p(co[0]),
-                              _p(co[1]), _p(co[2]), C, dy.p, dy.ld, s)
+                              _p(co[1]), _p(co[2]), C, dy.p, dy.ld, amax, s)
 
 
 def _sum_into(x: torch.Tensor, out: torch.Tensor, ws, stream: int):
@@ -629,6 +694,8 @@ class Workspace:
             else:
                 self.src[l.name] = self.dst[prev[l.name]]
         self.slab = E(self._slab_floats())
+        self.amax = torch.zeros(96, device=dev)   # h3 operand maxima, one slot per producer (UNetEngine._slot)
+        self.aslot = {}
         self.dpart = torch.empty(10 * 32768 + 4096, device=dev, dtype=torch.float64)
         self.sc_pending = None
         if train:

@@ -96,8 +96,10 @@ def get_engine(n_feat, n_cfeat, height, device, conv_math: str = "fp32") -> UNet
 
 
 def default_conv_math() -> str:
-    """3x3 conv arithmetic used when ContextUnet(conv_math=None): $CDM_CONV_MATH or "fp32"."""
-    return os.environ.get("CDM_CONV_MATH", "fp32")
+    """3x3 conv arithmetic used when ContextUnet(conv_math=None): $CDM_CONV_MATH or "h3" (fp32-class scaled
+    split-fp16 on the matrix cores; measured more accurate than "x6" and within 4x of torch's CPU fp32 conv
+    error, profiles/r1_conv_accuracy.jsonl).  "fp32" selects plain fp32 MFMA."""
+    return os.environ.get("CDM_CONV_MATH", "h3")
 
 
 def _stream() -> int:

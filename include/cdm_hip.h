@@ -46,9 +46,27 @@ int cdm_conv3x3_wgrad_x3(const float* dy, int lddy, int Cout, const float* x, in
                          int splits, float* slab, int nterm, void* stream);
 /* fp32 [K][N] (ld ldb) -> [ceil(K/16)][3][N][16] bf16 split terms hi/mid/lo */
 int cdm_split_bf16x3(const float* b, long long ldb, int K, int N, void* out, void* stream);
+/* fp32-class conv3x3 on the fp16 matrix cores ("h3"): each operand is scaled by a power of two derived
+ * from its max |.| (device scalars amax_x / amax_w, see cdm_amax_f32) and split into fp16 hi + lo;
+ * 3 cross products (hh, hl, lh) per MAC, fp32 accumulate, exact unscale.  wx from cdm_split_f16x2 of
+ * the packed weights with the same amax_w.  Same semantics as cdm_conv3x3_fwd. */
+int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
+                       const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags, float* stats,
+                       int stats_ld, int kc, float* amax_y, void* stream);
+int cdm_conv3x3_wgrad_h3(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,
+                         const float* amax_dy, const float* amax_x, int splits, float* slab, void* stream);
+/* fp32 [K][N] (ld ldb) -> [ceil(K/16)][3][N][16]: planes 0/1 = fp16 hi/lo of b * 2^(14-e), max|b| = *amax < 2^e */
+int cdm_split_f16x2(const float* b, long long ldb, int K, int N, const float* amax, void* out, void* stream);
+/* *out = max(accumulate ? *out : 0, max |x[r*ld + c]|), r < rows, c < C (atomic max, graph-capturable) */
+int cdm_amax_f32(const float* x, long long rows, int C, long long ld, float* out, int accumulate, void* stream);
+/* p[0..n) = 0 (hipMemsetAsync; graph-capturable) */
+int cdm_zero_f32(float* p, long long n, void* stream);
+/* Producers below (cdm_norm_apply_fwd / _bwd, cdm_convT2x2_fwd, cdm_conv3x3_fwd_h3 amax_y) take an optional
+ * float* amax: when non-null they atomically max the |values| they store into it, so the next h3 conv gets
+ * its operand's max without a separate pass. */
 /* nn.ConvTranspose2d(Cin,Cout,2,2) forward (diffusion_utilities.py:86); H,W = input grid. */
 int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk, const float* bias,
-                     float* y, int ldy, int Cout, void* stream);
+                     float* y, int ldy, int Cout, float* amax, void* stream);
 /* its input gradient (autograd of diffusion_utilities.py:86). */
 int cdm_convT2x2_dgrad(const float* dy, int N, int H, int W, int Cout, int lddy, const float* wpkT, float* dx,
                        int lddx, int Cin, int flags, void* stream);
@@ -100,11 +118,11 @@ int cdm_col_sum(const float* in, int N, int C, float* out, int accumulate, void*
  * (BN/GN apply diffusion_utilities.py:28-29; MaxPool2d :109; random shortcut :54-55; FiLM ContextUnet.py:57-58) */
 int cdm_norm_apply_fwd(int flags, const float* y, int ldy, int N, int H, int W, int C, const float* s, const float* t,
                        int sn, const float* film_a, int film_an, const float* film_b, int film_bn, const float* rx,
-                       const float* rw, const float* rb, int rsplit, float* out, int ldo, void* stream);
+                       const float* rw, const float* rb, int rsplit, float* out, int ldo, float* amax, void* stream);
 int cdm_norm_apply_bwd(int mode, const float* g, int ldg, const float* y, int ldy, int N, int H, int W, int C,
                        const float* s, const float* t, int sn, const float* mean, const float* invstd, int mn, int cpg,
                        const float* film_a, int film_an, const float* A, const float* B, const float* Cc, int cn,
-                       float* dy, int lddy, void* stream);
+                       float* dy, int lddy, float* amax, void* stream);
 
 /* ---- small ops (csrc/misc.hip) ---------------------------------------------------------------- */
 /* init_conv.conv1: Conv2d(1, nf, 3, 1, 1) (ContextUnet.py:14 -> diffusion_utilities.py:27) */

@@ -3,7 +3,7 @@
 C4 (bf16 mixed precision: bf16 MFMA operands, fp32 accumulate / master weights / activations / norms):
   the reduced operand precision (8-bit mantissa, relative rounding 2^-9) is the only difference from
   fp32, so the bar is the bf16 one:
-    forward eps         max|d| <= 2e-2 * max|ref|          (vs the fp32 oracle)
+    forward eps         max|d| vs the fp32 oracle within 1.5x that of the oracle under bf16 operand rounding
     parameter grads     vs an fp64 oracle, relative L2 per tensor: max and median over tensors within
                         1.5x of those of the oracle run with the same bf16 operand rounding (every
                         3x3 conv's input and weights rounded to bf16, fp32 accumulate).  The network is
@@ -122,8 +122,15 @@ def _grad_errors(nf, H, B, math, seed=4, emulate_bf16=False):
 
 # ------------------------------------------------------------------------------------------ C4 (bf16)
 def test_c4_bf16_forward_vs_oracle():
-    for train, eps, ref in _forward_pair(64, 64, 3, "bf16"):
-        assert _rel(eps, ref) < 2e-2, (train, _rel(eps, ref))
+    """bf16 forward vs the fp32 oracle: within 1.5x the error of the oracle itself under bf16 operand rounding
+    (train-mode BatchNorm amplifies operand noise: ~2 % of max|eps| for both on this input)."""
+    got = _forward_pair(64, 64, 3, "bf16")
+    with _bf16_operands():
+        emu = _forward_pair(64, 64, 3, "fp32")
+    for (train, eps, ref), (_, _, ref_bf) in zip(got, emu):
+        e_hip, e_emu = _rel(eps, ref), _rel(ref_bf, ref)
+        print("train" if train else "eval", "hip", e_hip, "oracle-bf16", e_emu)
+        assert e_hip <= max(1.5 * e_emu, 1e-3), (train, e_hip, e_emu)
 
 
 def test_c4_bf16_train_grads_vs_fp64():

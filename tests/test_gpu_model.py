@@ -1,7 +1,8 @@
 """Whole-model parity of the HIP ContextUnet against the CPU oracle / reference golden vectors.
 
-Every test runs with both 3x3-conv arithmetics: "fp32" (fp32 MFMA) and "x6" (fp32-accurate split-bf16
-MFMA, 6 cross terms) — same tolerances, so x6 is held to the fp32 bar.
+Every test runs with the three fp32-class 3x3-conv arithmetics: "fp32" (fp32 MFMA), "x6" (split-bf16
+MFMA, 6 cross terms) and "h3" (scaled split-fp16 MFMA, 3 cross terms) — same tolerances, so x6 and h3
+are held to the fp32 bar.
 
 Tolerances (fp32 everywhere; only summation order differs):
   forward eps            max|d| <= 1e-4 * max|ref|
@@ -27,7 +28,7 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-MATH = pytest.mark.parametrize("math", ["fp32", "x6"])
+MATH = pytest.mark.parametrize("math", ["fp32", "x6", "h3"])
 
 
 def _model(nf, ncf=6, sd=None, seed=0, math="fp32"):

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes (one counter group per pass, kernel-trace only) on the dominant conv in a given arithmetic.
-#   bash tools/pmc_x6.sh [x6|x3|x1|-1] [outdir]      (run from the repo root on the GPU box)
+#   bash tools/pmc_x6.sh [x6|h3|x3|x1|-1] [outdir]      (run from the repo root on the GPU box)
 set -e
 MODE=${1:-x6}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -62,7 +62,8 @@ def run(nf, H, T, B, math, steps, sample_n, sample_steps, ws=(0.0,)):
 if __name__ == "__main__":
     which = sys.argv[1]
     if which == "c4":
-        for math in ("bf16", "x3", "x6"):
+        maths = sys.argv[2].split(",") if len(sys.argv) > 2 else ["bf16", "x3", "x6"]
+        for math in maths:
             run(128, 64, 1500, 256, math, 10, 256, 50, ws=(0.0, 1.0, 3.0))
     elif which == "c5":
         B = int(sys.argv[2]) if len(sys.argv) > 2 else 4
