@@ -1322,6 +1322,18 @@ CDM_API int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int l
     return launch_gemm<LdDenseA, LdDenseB, EpiConvT2x2, false>(la, lb, ep, M, NN, K, 1, S(stream));
 }
 
+// the same on the fp16 matrix cores (h3: scaled hi/lo split, see split_terms); wx = cdm_split_f16x2 of wpk
+CDM_API int cdm_convT2x2_fwd_h3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx,
+                                const float* amax_x, const float* amax_w, const float* bias, float* y, int ldy,
+                                int Cout, float* amax_y, void* stream) {
+    if (Cin % 4 || Cout % 4 || !amax_x || !amax_w) return (int)hipErrorInvalidValue;
+    const int M = N * H * W, K = Cin, NN = 4 * Cout;
+    EpiConvT2x2 ep{y, ldy, bias, H, W, Cout, M, NN, amax_y};
+    return launch_gemm_x3<RowK<LdDenseA>::template T, StagePre, EpiConvT2x2, true>(
+        MkRowK<LdDenseA>{LdDenseA{x, ldx, M, K}, amax_x}, MkPre{reinterpret_cast<const __bf16*>(wx), NN, amax_w}, ep,
+        M, NN, K, 1, NT_H3, S(stream));
+}
+
 // dX[n,h,w,ci] (+)= sum_{ij,co} dY[n,2h+i,2w+j,co] * W[ci][co][ij];  H, W are the INPUT (small) grid
 CDM_API int cdm_convT2x2_dgrad(const float* dy, int N, int H, int W, int Cout, int lddy, const float* wpkT,
                                float* dx, int lddx, int Cin, int flags, void* stream) {

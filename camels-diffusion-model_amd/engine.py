@@ -169,6 +169,8 @@ class UNetEngine:
             wtT = self._buf(name + ".wtT", (4 * nf, cin))
             lb.cdm_pack_convT(_p(P[name + ".weight"]), cin, nf, 4, _p(wt), _p(wtT) if train else None, stream)
             self.pk[name + ".wt"], self.pk[name + ".wtT"] = wt, wtT
+            if self.nterm == NT_H3:
+                self._split(name + ".wt", cin, 4 * nf, stream)
         c0 = 2 * nf
         w0 = self._buf("up0.wt", (c0, self.KK0 * c0))
         w0T = self._buf("up0.wtT", (self.KK0 * c0, c0))
@@ -239,18 +241,21 @@ class UNetEngine:
             assert i < ws.amax.numel()
         return _p(ws.amax) + 4 * i
 
+    # producers writing slices of one concatenation buffer share that buffer's slot (its consumers read the
+    # whole buffer, or a slice whose max the shared slot bounds from above — harmless for the scale)
+    _CAT_SLOT = {"init_conv.conv2": "catO", "up2.model.2.conv2": "catO", "down1.model.1.conv2": "catU2",
+                 "up1.model.2.conv2": "catU2", "down2.model.1.conv2": "catU1"}
+
     def _dst_slot(self, ws, l: "LayerSpec"):
-        # catO's two producers (init_conv output x0, up2 output) share one slot: out.0 reads both halves
-        return self._slot(ws, "catO" if l.name in ("init_conv.conv2", "up2.model.2.conv2") else "z:" + l.name)
+        return self._slot(ws, self._CAT_SLOT.get(l.name, "z:" + l.name))
 
     def _src_slot(self, ws, l: "LayerSpec"):
-        special = {"down1.model.0.conv1": "catO", "down2.model.0.conv1": "z:down1.model.1.conv2",
+        special = {"down1.model.0.conv1": "catO", "down2.model.0.conv1": "catU2",
                    "up1.model.1.conv1": "yT1", "up2.model.1.conv1": "yT2"}
         if l.name in special:
             return self._slot(ws, special[l.name])
-        i = self.layers.index(l)
-        return self._slot(ws, "catO" if self.layers[i - 1].name in ("init_conv.conv2",) else
-                          "z:" + self.layers[i - 1].name)
+        prev = self.layers[self.layers.index(l) - 1]
+        return self._dst_slot(ws, prev)
 
     # ------------------------------------------------------------------------------------------
     def workspace(self, B: int, train: bool) -> "Workspace":
@@ -311,15 +316,13 @@ class UNetEngine:
         u1 = ws.catU1.sl(0, c0)
         lb.cdm_norm_apply_fwd(APPLY_FILM | APPLY_RELU, _p(ws.y0), c0, B, H2, H2, c0, _p(ws.gn0["scale"]),
                               _p(ws.gn0["shift"]), c0, _p(ce1), c0 if rows_c > 1 else 0, _p(te1),
-                              c0 if rows_t > 1 else 0, None, None, None, 0, u1.p, u1.ld, None, s)
+                              c0 if rows_t > 1 else 0, None, None, None, 0, u1.p, u1.ld, self._slot(ws, "catU1"), s)
         # ---------------- up1 ----------------
-        lb.cdm_convT2x2_fwd(ws.catU1.p, B, H2, H2, 4 * nf, 4 * nf, _p(self.pk["up1.model.0.wt"]),
-                            _p(P["up1.model.0.bias"]), _p(ws.yT1), nf, nf, self._slot(ws, "yT1"), s)
+        self.convT2x2(ws, "up1.model.0", ws.catU1, B, H2, 4 * nf, P, ws.yT1, "catU1", "yT1", s)
         for l in self.layers[10:14]:
             self._conv_bn_fwd(ws, P, l, s, x)
         # ---------------- up2 ----------------
-        lb.cdm_convT2x2_fwd(ws.catU2.p, B, H1, H1, 2 * nf, 2 * nf, _p(self.pk["up2.model.0.wt"]),
-                            _p(P["up2.model.0.bias"]), _p(ws.yT2), nf, nf, self._slot(ws, "yT2"), s)
+        self.convT2x2(ws, "up2.model.0", ws.catU2, B, H1, 2 * nf, P, ws.yT2, "catU2", "yT2", s)
         for l in self.layers[14:18]:
             self._conv_bn_fwd(ws, P, l, s, x)
         # ---------------- out ----------------
@@ -330,6 +333,17 @@ class UNetEngine:
                               None, 0, None, 0, None, None, None, 0, _p(ws.zO), nf, None, s)
         lb.cdm_conv3x3_cout1_fwd(_p(ws.zO), nf, B, H, H, nf, _p(P["out.3.weight"]), _p(P["out.3.bias"]), _p(eps), s)
         return eps
+
+    def convT2x2(self, ws, name, x: Act, B, Hin, cin, P, y, src_slot, dst_slot, s):
+        """ConvTranspose2d(cin, nf, 2, 2) (diffusion_utilities.py:86) of x [B,Hin,Hin,cin] into y [B,2Hin,2Hin,nf]."""
+        nf = self.nf
+        if self.nterm == NT_H3:
+            lib().cdm_convT2x2_fwd_h3(x.p, B, Hin, Hin, cin, x.ld, _p(self.pk[name + ".wt_x"]), self._slot(ws, src_slot),
+                                      _p(self.pk[name + ".wt_amax"]), _p(P[name + ".bias"]), _p(y), nf, nf,
+                                      self._slot(ws, dst_slot), s)
+        else:
+            lib().cdm_convT2x2_fwd(x.p, B, Hin, Hin, cin, x.ld, _p(self.pk[name + ".wt"]), _p(P[name + ".bias"]),
+                                   _p(y), nf, nf, self._slot(ws, dst_slot), s)
 
     def _conv_bn_fwd(self, ws, P, l: LayerSpec, s, x):
         lb = lib()
@@ -376,7 +390,7 @@ class UNetEngine:
         kind = ws.dst_kind[l.name]
         dst = ws.dst[l.name]
         C = l.cout
-        am = self._dst_slot(ws, l) if kind != "film" else None    # FiLM2 output feeds the fp32 ConvT
+        am = self._dst_slot(ws, l)
         if kind == "dense" or kind == "plain":
             lb.cdm_norm_apply_fwd(relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), 0, None, 0, None, 0, None, None,
                                   None, 0, dst.p, dst.ld, am, s)

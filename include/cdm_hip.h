@@ -67,6 +67,10 @@ int cdm_zero_f32(float* p, long long n, void* stream);
 /* nn.ConvTranspose2d(Cin,Cout,2,2) forward (diffusion_utilities.py:86); H,W = input grid. */
 int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int ldx, const float* wpk, const float* bias,
                      float* y, int ldy, int Cout, float* amax, void* stream);
+/* the same on the fp16 matrix cores (h3); wx = cdm_split_f16x2 of wpk [Cin][4*Cout] with max|wpk| = *amax_w */
+int cdm_convT2x2_fwd_h3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
+                        const float* amax_w, const float* bias, float* y, int ldy, int Cout, float* amax_y,
+                        void* stream);
 /* its input gradient (autograd of diffusion_utilities.py:86). */
 int cdm_convT2x2_dgrad(const float* dy, int N, int H, int W, int Cout, int lddy, const float* wpkT, float* dx,
                        int lddx, int Cin, int flags, void* stream);

@@ -123,6 +123,16 @@ def test_convT2x2(L, N, Hin, Cin, Cout):
     torch.cuda.synchronize()
     _close(_nchw(y, N, 2 * Hin, 2 * Hin, Cout), ref.detach())
     assert am.item() == y.abs().max().item()          # fused producer max (h3 operand scale)
+    # h3 forward (scaled fp16 hi/lo split on the matrix cores): same fp32 tolerance, fused max|y|
+    wx, amw = _split_h3(L, wt, Cin, 4 * Cout)
+    amx = _amax(L, xn, N * Hin * Hin, Cin)
+    y3 = torch.empty_like(y)
+    am3 = torch.zeros(1, device="cuda")
+    L.cdm_convT2x2_fwd_h3(xn.data_ptr(), N, Hin, Hin, Cin, Cin, wx.data_ptr(), amx.data_ptr(), amw.data_ptr(),
+                          bc.data_ptr(), y3.data_ptr(), Cout, Cout, am3.data_ptr(), _s())
+    torch.cuda.synchronize()
+    _close(_nchw(y3, N, 2 * Hin, 2 * Hin, Cout), ref.detach())
+    assert am3.item() == y3.abs().max().item()
     gyn = _nhwc(gy)
     dx = torch.empty(N * Hin * Hin, Cin, device="cuda")
     L.cdm_convT2x2_dgrad(gyn.data_ptr(), N, Hin, Hin, Cout, Cout, wtT.data_ptr(), dx.data_ptr(), Cin, Cin, 0, _s())
