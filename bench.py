@@ -243,7 +243,42 @@ def extra_configs(args, barrier):
                                         "img_per_s": round(B5 / (sms * 1e-3 * T5), 5), "extrapolated_to_T": True}}}
     del model
     torch.cuda.empty_cache()
+    out["stats_pk_pdf"] = stats_rate(args.sample_batch)
     return out
+
+
+def stats_rate(n: int):
+    """Sample-statistics row: P(k) (power_spectrum, ortho DFT + radial bins) and per-map PDF
+    (0.01 bins) of n 64x64 maps on the HIP kernels, next to the reference algorithm on the CPU (oracle, 8 maps)."""
+    import cdm_amd
+    from oracle import stats_ref as R
+    g = torch.Generator(device="cuda").manual_seed(5)
+    maps = torch.rand(n, 1, H, H, device="cuda", generator=g)
+    edges = torch.arange(0.0, 1.0 + 0.01, 0.01, dtype=torch.float64).numpy()
+    cdm_amd.power_spectra(maps); cdm_amd.pdfs(maps, edges)            # warm-up (bin geometry cached)
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        cdm_amd.power_spectra(maps)
+    torch.cuda.synchronize()
+    pk_ms = (time.perf_counter() - t0) / reps * 1e3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        cdm_amd.pdfs(maps, edges)
+    torch.cuda.synchronize()
+    pdf_ms = (time.perf_counter() - t0) / reps * 1e3
+    host = maps[:8, 0].cpu().numpy()
+    t0 = time.perf_counter()
+    for m in host:
+        R.power_spectrum(m, 1.0)
+        import numpy as np
+        np.histogram(m.ravel(), edges, density=True)
+    cpu_ms = (time.perf_counter() - t0) / len(host) * 1e3
+    return {"workload": f"P(k) (diffusion_utilities.py:302) + PDF (train_diffusion.py:205) of {n} maps 64x64",
+            "power_spectra_ms": round(pk_ms, 3), "pdf_ms": round(pdf_ms, 3),
+            "maps_per_s": round(n / ((pk_ms + pdf_ms) * 1e-3), 1),
+            "cpu_reference_ms_per_map": round(cpu_ms, 3), "cpu_sample": "8 maps, numpy (1 thread, the reference loop)"}
 
 
 def main():

@@ -9,9 +9,12 @@ from .diffusion import DDPM, GraphSampler, Schedule, denoise_add_noise, perturb_
 from .likelihood import (LikelihoodEvaluator, calculate_elbo_and_bpd, calculate_elbo_and_bpd_batch,  # noqa: F401
                          calculate_elbo_and_bpd_dataset, calculate_likelihood)
 from .model import ContextUnet, EmbedFC, ResidualConvBlock, UnetDown, UnetUp  # noqa: F401
+from .stats import (calculate_power_spectrum_2d, compare_distributions, compare_power_spectra,  # noqa: F401
+                    pdfs, power_spectra, power_spectrum)
 from .trainer import Trainer  # noqa: F401
 
 __all__ = ["ContextUnet", "EmbedFC", "ResidualConvBlock", "UnetDown", "UnetUp", "lib", "DDPM", "GraphSampler",
            "Schedule", "denoise_add_noise", "perturb_input", "sample_ddpm", "Trainer", "LikelihoodEvaluator",
            "calculate_likelihood", "calculate_elbo_and_bpd", "calculate_elbo_and_bpd_batch",
-           "calculate_elbo_and_bpd_dataset"]
+           "calculate_elbo_and_bpd_dataset", "power_spectrum", "power_spectra", "compare_power_spectra",
+           "calculate_power_spectrum_2d", "compare_distributions", "pdfs"]

@@ -484,6 +484,7 @@ struct StageRowK {
     float sc;
     typename LD::Row row[LDN];
     float4 r[LDN];
+    __device__ __forceinline__ float sc_of() const { return op_scale<NT>(amax); }
     __device__ __forceinline__ void init(int tid, int r0) {
         sc = op_scale<NT>(amax);
 #pragma unroll
@@ -492,6 +493,10 @@ struct StageRowK {
     __device__ __forceinline__ void gload(int tid, int kt) {
 #pragma unroll
         for (int i = 0; i < LDN; ++i) r[i] = ld.load(row[i], kt * XBK + (tid % 4) * 4);
+    }
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int i = 0; i < LDN; ++i) r[i] = f4zero();
     }
     __device__ __forceinline__ void sstore(int tid, __bf16* base) const {
 #pragma unroll
@@ -515,9 +520,14 @@ struct StagePre {
     float sc;
     int rr, kh; bool ok;
     uint4 r[NS];
+    __device__ __forceinline__ float sc_of() const { return op_scale<NT>(amax); }
     __device__ __forceinline__ void init(int tid, int r0) {
         sc = op_scale<NT>(amax);
         rr = r0 + (tid >> 1); kh = (tid & 1) * 8; ok = rr < rows;
+    }
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int t = 0; t < NS; ++t) r[t] = make_uint4(0, 0, 0, 0);
     }
     __device__ __forceinline__ void gload(int, int kt) {
 #pragma unroll
@@ -541,8 +551,13 @@ struct StageColK {
     typename LD::Col col;
     float r[8];
     // thread -> (row tid>>1, k-half tid&1): an 8-lane store group covers 4 rows x 2 halves (conflict-free)
+    __device__ __forceinline__ float sc_of() const { return op_scale<NT>(amax); }
     __device__ __forceinline__ void init(int tid, int r0) { sc = op_scale<NT>(amax); col = ld.col(r0 + (tid >> 1)); }
     __device__ __forceinline__ void gload(int tid, int kt) { ld.load8(col, kt * XBK + (tid & 1) * 8, r); }
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = 0.f;
+    }
     __device__ __forceinline__ void sstore(int tid, __bf16* base) const {
         __bf16 h[8], m[8], l[8];
         split_terms<NT>(r, sc, h, m, l);
@@ -555,13 +570,16 @@ struct StageColK {
     }
 };
 
-// SA: operand A stager (rows = M), SB: operand B stager (rows = N); split-K over blockIdx.z.
-template <class SA, class SB, class EP, int NT, bool XCD_REMAP>
-__global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa, SB sb, EP ep, int K, int kt_per_split) {
+// SA: operand A stager (rows = M), SB: operand B stager (rows = N); split-K over blockIdx.z.  KS 16-deep K
+// tiles share one barrier interval (one stager copy per tile; tiles past the split's end are zero-filled).
+// (KS = 2 measured: ConvT 2x2 fwd 602 -> 695 us, 64 KiB LDS costs a block per CU — KS = 1 ships)
+template <class SA, class SB, class EP, int NT, bool XCD_REMAP, int KS = 1>
+__global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa0, SB sb0, EP ep, int K, int kt_per_split) {
     constexpr int NS = XTerms<NT>::NS;
-    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * NS * XPLANE];
-    __bf16* As = smem;                        // [buf][term][row][16 k] (xoff swizzle)
-    __bf16* Bs = smem + 2 * NS * XPLANE;
+    constexpr int TILE = NS * XPLANE;                 // bf16 per operand per K tile
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * KS * TILE];
+    __bf16* As = smem;                        // [buf][ks][term][row][16 k] (xoff swizzle)
+    __bf16* Bs = smem + 2 * KS * TILE;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -583,55 +601,71 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa, SB sb, EP e
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    sa.init(tid, m0);
-    sb.init(tid, n0);
-    if (kt0 < kt1) {
-        sa.gload(tid, kt0); sb.gload(tid, kt0);
-        sa.sstore(tid, As); sb.sstore(tid, Bs);
+    SA sa[KS];
+    SB sb[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        sa[ks] = sa0; sb[ks] = sb0;
+        sa[ks].init(tid, m0); sb[ks].init(tid, n0);
     }
+    auto gload = [&](int kt) {          // K tiles kt .. kt+KS-1 (zeros past the split's end)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            if (kt + ks < kt1) { sa[ks].gload(tid, kt + ks); sb[ks].gload(tid, kt + ks); }
+            else { sa[ks].zero(); sb[ks].zero(); }
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            sa[ks].sstore(tid, As + (buf * KS + ks) * TILE);
+            sb[ks].sstore(tid, Bs + (buf * KS + ks) * TILE);
+        }
+    };
+    if (kt0 < kt1) { gload(kt0); sstore(0); }
     __syncthreads();
     int cur = 0;
     const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31), kh = (lane >> 5) * 8;
     int aoff[2], boff[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) { aoff[i] = xoff(ar + 32 * i, kh); boff[i] = xoff(br + 32 * i, kh); }
-    for (int kt = kt0; kt < kt1; ++kt) {
-        const bool more = kt + 1 < kt1;
-        if (more) { sa.gload(tid, kt + 1); sb.gload(tid, kt + 1); }
-        const __bf16* a = As + cur * NS * XPLANE;
-        const __bf16* b = Bs + cur * NS * XPLANE;
-        bf16x8 fa[2][NS], fb[2][NS];
+    for (int kt = kt0; kt < kt1; kt += KS) {
+        const bool more = kt + KS < kt1;
+        if (more) gload(kt + KS);
 #pragma unroll
-        for (int t = 0; t < NS; ++t)
+        for (int ks = 0; ks < KS; ++ks) {
+            const __bf16* a = As + (cur * KS + ks) * TILE;
+            const __bf16* b = Bs + (cur * KS + ks) * TILE;
+            bf16x8 fa[2][NS], fb[2][NS];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                fa[i][t] = *reinterpret_cast<const bf16x8*>(a + t * XPLANE + aoff[i]);
-                fb[i][t] = *reinterpret_cast<const bf16x8*>(b + t * XPLANE + boff[i]);
-            }
+            for (int t = 0; t < NS; ++t)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                f32x16 c = acc[i][j];
-                if constexpr (NT >= 6) {
-                    c = xmfma<NT>(fa[i][1], fb[j][1], c);   // mm
-                    c = xmfma<NT>(fa[i][2], fb[j][0], c);   // lh
-                    c = xmfma<NT>(fa[i][0], fb[j][2], c);   // hl
+                for (int i = 0; i < 2; ++i) {
+                    fa[i][t] = *reinterpret_cast<const bf16x8*>(a + t * XPLANE + aoff[i]);
+                    fb[i][t] = *reinterpret_cast<const bf16x8*>(b + t * XPLANE + boff[i]);
                 }
-                if constexpr (NT >= 3) {
-                    c = xmfma<NT>(fa[i][1], fb[j][0], c);   // mh (NT_H3: lo.hi)
-                    c = xmfma<NT>(fa[i][0], fb[j][1], c);   // hm (NT_H3: hi.lo)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    f32x16 c = acc[i][j];
+                    if constexpr (NT >= 6) {
+                        c = xmfma<NT>(fa[i][1], fb[j][1], c);   // mm
+                        c = xmfma<NT>(fa[i][2], fb[j][0], c);   // lh
+                        c = xmfma<NT>(fa[i][0], fb[j][2], c);   // hl
+                    }
+                    if constexpr (NT >= 3) {
+                        c = xmfma<NT>(fa[i][1], fb[j][0], c);   // mh (NT_H3: lo.hi)
+                        c = xmfma<NT>(fa[i][0], fb[j][1], c);   // hm (NT_H3: hi.lo)
+                    }
+                    acc[i][j] = xmfma<NT>(fa[i][0], fb[j][0], c);  // hh
                 }
-                acc[i][j] = xmfma<NT>(fa[i][0], fb[j][0], c);  // hh
-            }
-        if (more) {
-            sa.sstore(tid, As + (cur ^ 1) * NS * XPLANE);
-            sb.sstore(tid, Bs + (cur ^ 1) * NS * XPLANE);
         }
+        if (more) sstore(cur ^ 1);
         __syncthreads();
         cur ^= 1;
     }
-    unscale<NT>(acc, sa.sc, sb.sc);
+    unscale<NT>(acc, sa0.sc_of(), sb0.sc_of());
     ep(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
 }
 
@@ -689,7 +723,7 @@ template <class LD> struct ColK { template <int NT> using T = StageColK<LD, NT>;
 constexpr int HBM_ = 256;          // output pixels per block
 constexpr int HTHREADS = 512;
 
-template <int NT, int WT, class EP, bool XCD_REMAP>
+template <int NT, int WT, class EP, bool XCD_REMAP, bool PREFETCH = false>
 __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const float* __restrict__ x, int H, int Cin,
                                                                       int ldx, const __bf16* __restrict__ wx3,
                                                                       int Cout, const float* amax_x,
@@ -724,29 +758,32 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    // ---- halo staging: piece q = (halo pixel q>>2, channels 4(q&3)..+3) ----
+    // ---- halo staging: piece q = (halo pixel q>>2, channels 4(q&3)..+3); addresses fixed per block ----
     float4 hreg[HQ];
+    const float* hsrc[HQ];          // chunk-0 source of piece j (nullptr: zero padding / past the halo)
+    int hdst[HQ];                   // its LDS offset within a term plane
+#pragma unroll
+    for (int j = 0; j < HQ; ++j) {
+        const int q = tid + j * HTHREADS;
+        const int hp = q >> 2, c4 = q & 3;
+        const int hr = hp / HC, hc = hp - hr * HC;
+        const int ih = h0 - 1 + hr, iw = hc - 1;
+        hsrc[j] = (q < HPX * 4 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)WT)
+                      ? x + ((long long)(img * H + ih) * WT + iw) * ldx + c4 * 4 : nullptr;
+        hdst[j] = q < HPX * 4 ? xoff(hp, c4 * 4) : -1;
+    }
     auto gload_halo = [&](int cc) {
 #pragma unroll
-        for (int j = 0; j < HQ; ++j) {
-            const int q = tid + j * HTHREADS;
-            const int hp = q >> 2, c4 = q & 3;
-            const int hr = hp / HC, hc = hp - hr * HC;
-            const int ih = h0 - 1 + hr, iw = hc - 1;
-            hreg[j] = (q < HPX * 4 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)WT)
-                          ? ld4(x + ((long long)(img * H + ih) * WT + iw) * ldx + cc * 16 + c4 * 4)
-                          : f4zero();
-        }
+        for (int j = 0; j < HQ; ++j) hreg[j] = hsrc[j] ? ld4(hsrc[j] + cc * 16) : f4zero();
     };
     auto store_halo = [&](__bf16* base) {
 #pragma unroll
         for (int j = 0; j < HQ; ++j) {
-            const int q = tid + j * HTHREADS;
-            if (q < HPX * 4) {
+            if (hdst[j] >= 0) {
                 const float xv[4] = {hreg[j].x, hreg[j].y, hreg[j].z, hreg[j].w};
                 __bf16 h[4], m[4], l[4];
                 split_terms<NT>(xv, sx, h, m, l);
-                __bf16* d = base + xoff(q >> 2, (q & 3) * 4);
+                __bf16* d = base + hdst[j];
                 *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
                 if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + HPLANE) = bf16x4{m[0], m[1], m[2], m[3]};
                 if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + 2 * HPLANE) = bf16x4{l[0], l[1], l[2], l[3]};
@@ -791,24 +828,38 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     int boff[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) boff[j] = xoff(wn * 64 + 32 * j + (lane & 31), kh);
+    int aoff[3][3][2];              // A fragment offset of tap (dy, dx), row block i (fixed per lane)
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) aoff[dy][dx][i] = xoff(hp0[i] + dy * HC + dx, kh);
 
     // the 3 taps (dx) of kernel row dy of the current chunk: fragments from the halo image a and B group b
     auto compute = [&](int dy, const __bf16* a, const __bf16* b) {
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-            // term-major: the hi fragments are read first and the hh products issue while the mid / lo
-            // fragments are still in flight
-            bf16x8 fa[2][NS], fb[2][NS];
-            int ao[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) ao[i] = xoff(hp0[i] + dy * HC + dx, kh);
+        // register double buffer: the fragments of tap dx+1 are read while the MFMAs of tap dx issue
+        bf16x8 FA[2][2][NS], FB[2][2][NS];
+        auto ldfrag = [&](int buf, int dx) {
 #pragma unroll
             for (int t = 0; t < NS; ++t)
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    fa[i][t] = *reinterpret_cast<const bf16x8*>(a + t * HPLANE + ao[i]);
-                    fb[i][t] = *reinterpret_cast<const bf16x8*>(b + (dx * NS + t) * XPLANE + boff[i]);
+                    FA[buf][i][t] = *reinterpret_cast<const bf16x8*>(a + t * HPLANE + aoff[dy][dx][i]);
+                    FB[buf][i][t] = *reinterpret_cast<const bf16x8*>(b + (dx * NS + t) * XPLANE + boff[i]);
                 }
+        };
+        if constexpr (PREFETCH) ldfrag(0, 0);
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+            if constexpr (PREFETCH) {
+                if (dx < 2) ldfrag((dx + 1) & 1, dx + 1);
+            } else {
+                ldfrag(dx & 1, dx);
+            }
+            const auto& fa = FA[dx & 1];
+            const auto& fb = FB[dx & 1];
+            // term-major: the hh products issue first, the cross terms after
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -832,6 +883,21 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
                         acc[i][j] = xmfma<NT>(fa[i][2], fb[j][0], acc[i][j]);
                     }
             }
+        }
+        if constexpr (PREFETCH) {
+            // pin the interleave: the next tap's fragment reads go one per MFMA gap of the current tap
+            constexpr int MF = 4 * (NT >= 6 ? 6 : (NT >= 3 ? 3 : 1)), RD = 4 * NS;
+            __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);          // tap 0 fragments
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) {
+#pragma unroll
+                for (int k = 0; k < RD; ++k) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, MF - RD, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);          // last tap
         }
     };
 
@@ -858,13 +924,12 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregB);
         __syncthreads();
         bb ^= 1;
-        // dy = 2: fetch B of the next chunk's dy = 0; store it and the next halo (buffer idle since chunk cc-1)
+        // dy = 2: fetch B of the next chunk's dy = 0; split + store the next halo (buffer idle since chunk cc-1)
+        // ahead of this group's MFMAs, so its VALU work interleaves with them; B after them (just issued)
         if (morec) gload_b(g0 + 3, bregA);
+        if (morec) store_halo(Hs + (hb ^ 1) * NS * HPLANE);
         compute(2, a, Bs + bb * BPL * XPLANE);
-        if (morec) {
-            store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregA);
-            store_halo(Hs + (hb ^ 1) * NS * HPLANE);
-        }
+        if (morec) store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregA);
         __syncthreads();
         bb ^= 1;
         hb ^= 1;
@@ -881,13 +946,13 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 // and the k-contiguous MFMA fragments are produced by the hardware transpose read ds_read_b64_tr_b16
 // (two per fragment).  Block: 128 co x 128 columns of one tap (Cin % 128 == 0, Cout % 128 == 0), 4 waves
 // 2x2 of 64x64, split-K over blockIdx.z.  The 16 pixels of a K step lie in one image row (W % 16 == 0),
-// so the tap shift is one bounds test per pixel.
+// so the tap shift is one bounds test per pixel.  KS K steps (16 pixels each) share one barrier interval.
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 static __device__ __forceinline__ int trswz(int row, int ch) {   // byte offset of 16-B chunk ch in row
     return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
 }
 
-template <int NT>
+template <int NT, int KS = 1>   // KS = 2 measured neutral (1.06 vs 1.07 ms per 309 GF)
 __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float* __restrict__ dy, int lddy, int Cout,
                                                                      const float* __restrict__ x, int H, int W, int Cin,
                                                                      int ldx, int K, int kt_per_split,
@@ -895,7 +960,8 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
                                                                      EpiStore ep) {
     constexpr int NS = XTerms<NT>::NS;
     constexpr int IMG = 16 * 128;                     // bf16 per [16 pix][128 ch] term image
-    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * NS * IMG];
+    constexpr int STEP = 2 * NS * IMG;                // bf16 per K step (both operands, all terms)
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * KS * STEP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     // 1-D grid, split-major logical order L = z*T + tile, remapped so that each XCD (hardware block b -> XCD b%8)
@@ -929,27 +995,34 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
     // running image coordinates of the K step's first pixel
     int p0 = kt0 * 16;
     int pn = p0 / hw, ph = (p0 - pn * hw) / W, pw = p0 - pn * hw - ph * W;
-    float4 ra[2], rb[2];
-    auto gload = [&]() {
+    float4 ra[KS][2], rb[KS][2];
+    auto gload = [&](int kt) {          // the KS K steps from kt (zero past kt1)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int kk = kq + 8 * i;
-            const long long pix = (long long)(pn * H + ph) * W + pw + kk;
-            ra[i] = ld4(dy + pix * lddy + m0 + c4);
-            const int hh = ph + sdy, ww = pw + kk + sdx;
-            rb[i] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
-                        ? ld4(x + ((long long)(pn * H + hh) * W + ww) * ldx + ci0 + c4)
-                        : f4zero();
+        for (int ks = 0; ks < KS; ++ks) {
+            const bool ok = kt + ks < kt1;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int kk = kq + 8 * i;
+                const long long pix = (long long)(pn * H + ph) * W + pw + kk;
+                ra[ks][i] = ok ? ld4(dy + pix * lddy + m0 + c4) : f4zero();
+                const int hh = ph + sdy, ww = pw + kk + sdx;
+                rb[ks][i] = (ok && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                                ? ld4(x + ((long long)(pn * H + hh) * W + ww) * ldx + ci0 + c4)
+                                : f4zero();
+            }
+            pw += 16;
+            if (pw >= W) { pw = 0; if (++ph == H) { ph = 0; ++pn; } }
         }
-        pw += 16;
-        if (pw >= W) { pw = 0; if (++ph == H) { ph = 0; ++pn; } }
     };
-    auto sstore = [&](__bf16* base) {
+    auto sstore = [&](__bf16* base0) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
         for (int op = 0; op < 2; ++op)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const float4 v = op ? rb[i] : ra[i];
+                __bf16* base = base0 + ks * STEP;
+                const float4 v = op ? rb[ks][i] : ra[ks][i];
                 const float xv[4] = {v.x, v.y, v.z, v.w};
                 __bf16 h[4], m[4], l[4];
                 split_terms<NT>(xv, op ? sx_ : sdy_, h, m, l);
@@ -974,13 +1047,15 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
         }
     }
 
-    if (kt0 < kt1) { gload(); sstore(smem); }
+    if (kt0 < kt1) { gload(kt0); sstore(smem); }
     __syncthreads();
     int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-        const bool more = kt + 1 < kt1;
-        if (more) gload();
-        const char* a = reinterpret_cast<const char*>(smem + cur * 2 * NS * IMG);
+    for (int kt = kt0; kt < kt1; kt += KS) {
+        const bool more = kt + KS < kt1;
+        if (more) gload(kt + KS);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+        const char* a = reinterpret_cast<const char*>(smem + (cur * KS + ks) * STEP);
         const char* b = a + NS * IMG * 2;
         bf16x8 fa[2][NS], fb[2][NS];
 #pragma unroll
@@ -1010,7 +1085,8 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
                 }
                 acc[i][j] = xmfma<NT>(fa[i][0], fb[j][0], c);
             }
-        if (more) sstore(smem + (cur ^ 1) * 2 * NS * IMG);
+        }
+        if (more) sstore(smem + (cur ^ 1) * KS * STEP);
         __syncthreads();
         cur ^= 1;
     }

@@ -194,6 +194,10 @@ def main(argv=None):
         np.save(os.path.join(out_dir, "reconstructed_images.npy"), rec.cpu().numpy())
         np.save(os.path.join(out_dir, "intermediate.npy"), inter)
         log.write(f"Reconstruction of {ns} maps, T={a.timesteps}: {dt:.2f} s\n")
+        # the reference's post-sampling statistics (code/train_diffusion.py:250, diffusion_utilities.py:370),
+        # on the HIP statistics kernels; the plotted arrays go to .npz files
+        cdm_amd.compare_distributions(x[:, 0].cpu().numpy(), rec[:, 0].cpu().numpy(), out_dir)
+        cdm_amd.compare_power_spectra(x, rec, out_dir)
         if conditional:
             t0 = time.time()
             samples, _ = d.sample_ddpm(ns, H, dev, p, a.guide_w)

@@ -59,6 +59,18 @@ int cdm_conv3x3_wgrad_h3(const float* dy, int lddy, int Cout, const float* x, in
 int cdm_split_f16x2(const float* b, long long ldb, int K, int N, const float* amax, void* out, void* stream);
 /* *out = max(accumulate ? *out : 0, max |x[r*ld + c]|), r < rows, c < C (atomic max, graph-capturable) */
 int cdm_amax_f32(const float* x, long long rows, int C, long long ld, float* out, int accumulate, void* stream);
+/* ---- sample statistics (csrc/stats.hip) --------------------------------------------------------
+ * power[b][u][v] = |sum_{x,y} img[b][x][y] e^{-2 pi i (u x + v y) / N}|^2 * scale, fp64 (direct DFT; T = scratch of
+ * B*N*N complex doubles).  scale 1/N^2 = np.fft.fftn(norm="ortho") of power_spectrum, diffusion_utilities.py:322;
+ * scale 1 = np.fft.fft2 of calculate_power_spectrum_2d, sample_power_spectra.py:128. */
+int cdm_dft2_power(const float* img, int B, int N, double scale, void* T, double* power, void* stream);
+/* out[b][k] = sum_{i = off[k]}^{off[k+1]-1} power[b][idx[i]] in list order (the reference's binning loops,
+ * diffusion_utilities.py:352-356 / sample_power_spectra.py:157-163, with the bin geometry built on the host) */
+int cdm_bin_sum(const double* power, int B, long long NN, const int* off, const int* idx, int nbins, double* out,
+                void* stream);
+/* out[b] = np.histogram(x[b], edges[0..nbins], density=True)[0]  (train_diffusion.py:205-207) */
+int cdm_histogram_density(const float* x, int B, long long P, const double* edges, int nbins, double* out,
+                          void* stream);
 /* p[0..n) = 0 (hipMemsetAsync; graph-capturable) */
 int cdm_zero_f32(float* p, long long n, void* stream);
 /* Producers below (cdm_norm_apply_fwd / _bwd, cdm_convT2x2_fwd, cdm_conv3x3_fwd_h3 amax_y) take an optional

@@ -29,6 +29,10 @@ def test_cli_trains_checkpoints_and_samples(tmp_path, args, cond):
     assert ckpts == (["model_epoch_2.pth"] if cond else [])
     rec = np.load(out / "reconstructed_images.npy")
     assert rec.shape == (3, 1, 64, 64) and np.isfinite(rec).all()
+    pdf = np.load(out / "distribution_comparison.npz")          # train_diffusion.py:250 statistics
+    assert pdf["train_pdf_mean"].shape == pdf["bin_mid"].shape
+    pk = np.load(out / "power_spectrum_comparison.npz")
+    assert pk["k"].shape == (47,) and np.isfinite(pk["gen_mean"]).all()
     if cond:
         sd = torch.load(out / "weights" / "model_epoch_2.pth", weights_only=True)
         assert len(sd) == 156

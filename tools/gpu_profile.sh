@@ -11,7 +11,7 @@ MODE=${2:-x6}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- \
-    python3 $R/bench.py --steps 20 --warmup 5 --sample-steps 100 --no-cpu --conv-math $MODE \
+    python3 $R/bench.py --steps 20 --warmup 5 --sample-steps 100 --no-cpu --no-extra --conv-math $MODE \
     > $OUT/bench_under_rocprof.json 2> $OUT/trace.err
 rm -f $OUT/trace/bench_kernel_trace.csv
 timeout -k 10 900 bash $R/tools/pmc_x6.sh $MODE ${1:-gpurun_out/prof}/pmc > /dev/null
