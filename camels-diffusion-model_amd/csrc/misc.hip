@@ -213,6 +213,91 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_kernel(const float* z, int
     }
 }
 
+// Band form (W | 256, C % 16 == 0): a block owns R = 256/W whole output rows of one image.  The R + 2 input
+// rows of the band are staged through LDS 16 channels at a time (coalesced 64-byte pixel pieces); each thread
+// reduces its halo pixels to the 9 per-tap partial sums s[tap][q] = sum_c z[q][c] w[c][tap] (the weights are
+// wave-uniform: scalar loads), and every output pixel then adds its 9 neighbours' partials.  z is read from
+// HBM once (+2/R halo rows) instead of 9 times through the caches.
+__global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* __restrict__ z, int ldz, int H, int W,
+                                                                  int C, const float* __restrict__ w,
+                                                                  const float* __restrict__ bias,
+                                                                  float* __restrict__ out) {
+    constexpr int HPMAX = 512;                        // (R + 2) * W <= 256 + 2 * 128 for W <= 128; W = 256 -> 768
+    __shared__ float zt[3 * 256 * 17];                // [halo px][16 ch + 1 pad]
+    __shared__ float st[9 * 3 * 256];                 // [tap][halo px]
+    const int R = 256 / W, HP = (R + 2) * W;
+    const int bands = H / R, n = blockIdx.x / bands, h0 = (blockIdx.x - n * bands) * R;
+    const int tid = threadIdx.x;
+    (void)HPMAX;
+    float acc[3][9];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[k][t] = 0.f;
+    // staging: piece i of this thread = (halo pixel q4>>2, channels 4(q4&3)..+3) of the current 16-channel slab;
+    // the next slab's pieces are loaded into registers while this slab is reduced (one slab of latency hidden)
+    constexpr int PQ = 12;                            // (768 * 4) / 256
+    const float* src[PQ];
+#pragma unroll
+    for (int i = 0; i < PQ; ++i) {
+        const int q4 = tid + i * 256, q = q4 >> 2, part = q4 & 3;
+        const int hh = h0 - 1 + q / W, ww = q - (q / W) * W;
+        src[i] = (q < HP && (unsigned)hh < (unsigned)H) ? z + (((long long)n * H + hh) * W + ww) * ldz + part * 4
+                                                        : nullptr;
+    }
+    float4 pre[PQ];
+    auto gload = [&](int c0) {
+#pragma unroll
+        for (int i = 0; i < PQ; ++i) pre[i] = src[i] ? ld4(src[i] + c0) : f4zero();
+    };
+    gload(0);
+    for (int c0 = 0; c0 < C; c0 += 16) {
+#pragma unroll
+        for (int i = 0; i < PQ; ++i) {
+            const int q4 = tid + i * 256;
+            if ((q4 >> 2) < HP) {
+                float* d = zt + (q4 >> 2) * 17 + (q4 & 3) * 4;
+                d[0] = pre[i].x; d[1] = pre[i].y; d[2] = pre[i].z; d[3] = pre[i].w;
+            }
+        }
+        __syncthreads();
+        if (c0 + 16 < C) gload(c0 + 16);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int q = tid + k * 256;
+            if (q < HP) {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) {
+                    const float v = zt[q * 17 + c];
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) acc[k][t] = fmaf(v, w[(c0 + c) * 9 + t], acc[k][t]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int q = tid + k * 256;
+        if (q < HP) {
+#pragma unroll
+            for (int t = 0; t < 9; ++t) st[t * HP + q] = acc[k][t];
+        }
+    }
+    __syncthreads();
+    // output pixel (h0 + r, c): sum over taps of the partial of halo pixel (r + ky, c + kx - 1)
+    const int r = tid / W, c = tid - r * W;
+    float o = bias[0];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            const int cc = c + kx - 1;
+            if ((unsigned)cc < (unsigned)W) o += st[(ky * 3 + kx) * HP + (r + ky) * W + cc];
+        }
+    out[((long long)n * H + h0 + r) * W + c] = o;
+}
+
 // dz[p'][ci] = sum_tap deps[p' - tap + 1] * w[ci][tap]   (lanes span channels, deps taps broadcast)
 __global__ __launch_bounds__(256) void conv_cout1_dgrad_kernel(const float* deps, int N, int H, int W, int C,
                                                                const float* w, float* dz, int lddz) {
@@ -619,6 +704,11 @@ CDM_API int cdm_conv3x3_cout1_fwd(const float* z, int ldz, int N, int H, int W, 
                                   float* out, void* stream) {
     if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
     const long long P = (long long)N * H * W;
+    if (C % 16 == 0 && W <= 256 && 256 % W == 0 && H % (256 / W) == 0 && ldz % 4 == 0) {
+        hipLaunchKernelGGL(conv_cout1_fwd_band_kernel, dim3(N * (H / (256 / W))), dim3(256), 0, S(stream), z, ldz, H, W,
+                           C, w, bias, out);
+        return cdm_status();
+    }
     hipLaunchKernelGGL(conv_cout1_fwd_kernel, dim3(nblocks(P, 256 / (C / 4), 8192)), dim3(256), 0, S(stream), z, ldz, N, H,
                        W, C, w, bias, out);
     return cdm_status();
