@@ -631,6 +631,30 @@ __global__ void pack_conv3x3_kernel(const float* W, const float* b, int Cin, int
 }
 
 // ConvTranspose weight W[ci][co][kk] ->  wt[ci][kk*Cout + co],  wtT[(kk*Cout + co)][ci]
+// out[b][c][r] = in[b][r][c] for `batch` R x C matrices: 64 x 64 tiles through LDS (reads coalesced along c,
+// writes along r; the +1 pad keeps the column reads conflict-free)
+__global__ __launch_bounds__(256) void transpose_tiled_kernel(const float* __restrict__ in, long long R, long long C,
+                                                              float* __restrict__ out) {
+    __shared__ float t[64][65];
+    const long long tilesC = (C + 63) / 64;
+    const long long b = blockIdx.y;
+    const long long r0 = (blockIdx.x / tilesC) * 64, c0 = (blockIdx.x % tilesC) * 64;
+    const float* ib = in + b * R * C;
+    float* ob = out + b * R * C;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const long long r = r0 + ty + 4 * k, c = c0 + tx;
+        if (r < R && c < C) t[ty + 4 * k][tx] = ib[r * C + c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const long long c = c0 + ty + 4 * k, r = r0 + tx;
+        if (r < R && c < C) ob[c * R + r] = t[tx][ty + 4 * k];
+    }
+}
+
 __global__ void pack_convT_kernel(const float* W, int Cin, int Cout, int KK, float* wt, float* wtT) {
     const long long total = (long long)Cin * Cout * KK;
     for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -642,16 +666,6 @@ __global__ void pack_convT_kernel(const float* W, int Cin, int Cout, int KK, flo
         const long long col = (long long)kk * Cout + co;
         if (wt) wt[(long long)ci * KK * Cout + col] = v;
         if (wtT) wtT[col * Cin + ci] = v;
-    }
-}
-
-// out[c][r] = in[r][c]
-__global__ void transpose_kernel(const float* in, int R, int C, float* out) {
-    const long long total = (long long)R * C;
-    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (long long)gridDim.x * blockDim.x) {
-        const int r = (int)(idx / C), c = (int)(idx - (long long)r * C);
-        out[(long long)c * R + r] = in[idx];
     }
 }
 
@@ -807,13 +821,26 @@ CDM_API int cdm_pack_conv3x3(const float* W, const float* b, int Cin, int Cout, 
                        Cout, gamma, beta, rm, rv, eps, wpk, bpk, wdg, kc);
     return cdm_status();
 }
+static void transpose_tiled(const float* in, long long batch, long long R, long long C, float* out, hipStream_t s) {
+    const long long tiles = ((R + 63) / 64) * ((C + 63) / 64);
+    hipLaunchKernelGGL(transpose_tiled_kernel, dim3((unsigned)tiles, (unsigned)batch), dim3(256), 0, s, in, R, C, out);
+}
+
 CDM_API int cdm_pack_convT(const float* W, int Cin, int Cout, int KK, float* wt, float* wtT, void* stream) {
+    if (wt) {
+        // wt[ci] = W[ci]^T  ([Cout][KK] -> [KK][Cout]);  wtT = wt^T ([Cin][KK*Cout] -> [KK*Cout][Cin])
+        if (KK > 1) transpose_tiled(W, Cin, Cout, KK, wt, S(stream));
+        else if (hipMemcpyAsync(wt, W, sizeof(float) * (size_t)Cin * Cout, hipMemcpyDeviceToDevice, S(stream)) != hipSuccess)
+            return cdm_status();
+        if (wtT) transpose_tiled(wt, 1, Cin, (long long)KK * Cout, wtT, S(stream));
+        return cdm_status();
+    }
     hipLaunchKernelGGL(pack_convT_kernel, dim3(nblocks((long long)Cin * Cout * KK)), dim3(256), 0, S(stream), W, Cin, Cout,
                        KK, wt, wtT);
     return cdm_status();
 }
 CDM_API int cdm_transpose(const float* in, int R, int C, float* out, void* stream) {
-    hipLaunchKernelGGL(transpose_kernel, dim3(nblocks((long long)R * C)), dim3(256), 0, S(stream), in, R, C, out);
+    transpose_tiled(in, 1, R, C, out, S(stream));
     return cdm_status();
 }
 __global__ void counter_add_kernel(int* c, int d) { if (threadIdx.x == 0) *c += d; }
