@@ -723,7 +723,12 @@ template <class LD> struct ColK { template <int NT> using T = StageColK<LD, NT>;
 constexpr int HBM_ = 256;          // output pixels per block
 constexpr int HTHREADS = 512;
 
-template <int NT, int WT, class EP, bool XCD_REMAP, bool PREFETCH = false>
+// ABL: timing-ablation bits for tools/conv_ablation.py (1 = shipped for NS <= 2; x6 keeps 0: its registers do not fit
+// the second fragment set): 1 fragment prefetch (the next
+// tap's fragments are read during the current tap's MFMAs: 0.94 -> 0.84 ms), 2 every MFMA issued twice, 4 B
+// staged once (stale afterwards), 8 halo stored without the term split, 16 no barriers in the main loop,
+// 32 halo loaded for the first chunk only
+template <int NT, int WT, class EP, bool XCD_REMAP, int ABL = (NT >= 6 ? 0 : 1)>
 __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const float* __restrict__ x, int H, int Cin,
                                                                       int ldx, const __bf16* __restrict__ wx3,
                                                                       int Cout, const float* amax_x,
@@ -773,6 +778,9 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         hdst[j] = q < HPX * 4 ? xoff(hp, c4 * 4) : -1;
     }
     auto gload_halo = [&](int cc) {
+        if constexpr (ABL & 32) {
+            if (cc > 0) return;
+        }
 #pragma unroll
         for (int j = 0; j < HQ; ++j) hreg[j] = hsrc[j] ? ld4(hsrc[j] + cc * 16) : f4zero();
     };
@@ -782,7 +790,16 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
             if (hdst[j] >= 0) {
                 const float xv[4] = {hreg[j].x, hreg[j].y, hreg[j].z, hreg[j].w};
                 __bf16 h[4], m[4], l[4];
-                split_terms<NT>(xv, sx, h, m, l);
+                if constexpr (ABL & 8) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        h[e] = __builtin_bit_cast(__bf16, (unsigned short)__float_as_uint(xv[e]));
+                        m[e] = __builtin_bit_cast(__bf16, (unsigned short)(__float_as_uint(xv[e]) >> 16));
+                        l[e] = h[e];
+                    }
+                } else {
+                    split_terms<NT>(xv, sx, h, m, l);
+                }
                 __bf16* d = base + hdst[j];
                 *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
                 if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + HPLANE) = bf16x4{m[0], m[1], m[2], m[3]};
@@ -807,7 +824,11 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
                           : make_uint4(0, 0, 0, 0);
         }
     };
+    int bstores = 0;
     auto store_b = [&](__bf16* base, const uint4 (&breg)[BQ]) {
+        if constexpr (ABL & 4) {
+            if (bstores++ >= 2) return;
+        }
 #pragma unroll
         for (int j = 0; j < BQ; ++j) {
             const int q = tid + j * HTHREADS;
@@ -836,6 +857,10 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 #pragma unroll
             for (int i = 0; i < 2; ++i) aoff[dy][dx][i] = xoff(hp0[i] + dy * HC + dx, kh);
 
+    auto hmfma = [&](const bf16x8& fa_, const bf16x8& fb_, const f32x16& c_) {
+        if constexpr (ABL & 2) return xmfma<NT>(fa_, fb_, xmfma<NT>(fa_, fb_, c_));
+        else return xmfma<NT>(fa_, fb_, c_);
+    };
     // the 3 taps (dx) of kernel row dy of the current chunk: fragments from the halo image a and B group b
     auto compute = [&](int dy, const __bf16* a, const __bf16* b) {
         // register double buffer: the fragments of tap dx+1 are read while the MFMAs of tap dx issue
@@ -849,6 +874,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
                     FB[buf][i][t] = *reinterpret_cast<const bf16x8*>(b + (dx * NS + t) * XPLANE + boff[i]);
                 }
         };
+        constexpr bool PREFETCH = ABL & 1;
         if constexpr (PREFETCH) ldfrag(0, 0);
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) {
@@ -863,14 +889,14 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = xmfma<NT>(fa[i][0], fb[j][0], acc[i][j]);
+                for (int j = 0; j < 2; ++j) acc[i][j] = hmfma(fa[i][0], fb[j][0], acc[i][j]);
             if constexpr (NT >= 3) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        acc[i][j] = xmfma<NT>(fa[i][0], fb[j][1], acc[i][j]);
-                        acc[i][j] = xmfma<NT>(fa[i][1], fb[j][0], acc[i][j]);
+                        acc[i][j] = hmfma(fa[i][0], fb[j][1], acc[i][j]);
+                        acc[i][j] = hmfma(fa[i][1], fb[j][0], acc[i][j]);
                     }
             }
             if constexpr (NT >= 6) {
@@ -878,9 +904,9 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        acc[i][j] = xmfma<NT>(fa[i][1], fb[j][1], acc[i][j]);
-                        acc[i][j] = xmfma<NT>(fa[i][0], fb[j][2], acc[i][j]);
-                        acc[i][j] = xmfma<NT>(fa[i][2], fb[j][0], acc[i][j]);
+                        acc[i][j] = hmfma(fa[i][1], fb[j][1], acc[i][j]);
+                        acc[i][j] = hmfma(fa[i][0], fb[j][2], acc[i][j]);
+                        acc[i][j] = hmfma(fa[i][2], fb[j][0], acc[i][j]);
                     }
             }
         }
@@ -901,6 +927,9 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         }
     };
 
+    auto sync = [&]() {
+        if constexpr (!(ABL & 16)) __syncthreads();
+    };
     gload_halo(0);
     gload_b(0, bregA);
     store_halo(Hs);
@@ -917,12 +946,12 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         if (morec) gload_halo(cc + 1);
         compute(0, a, Bs + bb * BPL * XPLANE);
         store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregA);
-        __syncthreads();
+        sync();
         bb ^= 1;
         // dy = 1
         compute(1, a, Bs + bb * BPL * XPLANE);
         store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregB);
-        __syncthreads();
+        sync();
         bb ^= 1;
         // dy = 2: fetch B of the next chunk's dy = 0; split + store the next halo (buffer idle since chunk cc-1)
         // ahead of this group's MFMAs, so its VALU work interleaves with them; B after them (just issued)
@@ -930,7 +959,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         if (morec) store_halo(Hs + (hb ^ 1) * NS * HPLANE);
         compute(2, a, Bs + bb * BPL * XPLANE);
         if (morec) store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregA);
-        __syncthreads();
+        sync();
         bb ^= 1;
         hb ^= 1;
     }
@@ -1288,6 +1317,38 @@ static int conv3x3_fwd_split(const float* x, int N, int H, int W, int Cin, int l
     using LA = LdIm2colA<0, 0>;
     return launch_gemm_x3<RowK<LA>::template T, StagePre, EpiStore, true>(
         MkRowK<LA>{LA{x, H, W, Cin, ldx, M, K}, amax_x}, mb, ep, M, Cout, K, 1, nterm, st);
+}
+
+// timing ablations of the h3 LDS-halo kernel (W = H = 64, kc = 16; tools/conv_ablation.py only)
+CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int Cin, int ldx, const void* wx,
+                                    const float* amax_x, const float* amax_w, float* y, int ldy, int Cout,
+                                    void* stream) {
+    if (H != 64 || Cin % 16 || ldx % 4) return (int)hipErrorInvalidValue;
+    const int M = N * H * 64;
+    const EpiStoreW<4> eh{y, ldy, 0, nullptr, Cout, 0, nullptr, 0, M, Cout};
+    const __bf16* b = reinterpret_cast<const __bf16*>(wx);
+    dim3 grid(M / HBM_, (Cout + GBN - 1) / GBN, 1);
+    hipStream_t s = S(stream);
+#define CDM_ABL(A) hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, 64, EpiStoreW<4>, true, A>), grid, dim3(HTHREADS), 0, \
+                                      s, x, H, Cin, ldx, b, Cout, amax_x, amax_w, eh)
+    switch (abl) {
+        case 0: CDM_ABL(0); break;
+        case 1: CDM_ABL(1); break;
+        case 2: CDM_ABL(2); break;
+        case 4: CDM_ABL(4); break;
+        case 8: CDM_ABL(8); break;
+        case 12: CDM_ABL(12); break;
+        case 14: CDM_ABL(14); break;
+        case 16: CDM_ABL(16); break;
+        case 32: CDM_ABL(32); break;
+        case 17: CDM_ABL(17); break;
+        case 60: CDM_ABL(60); break;
+        case 61: CDM_ABL(61); break;
+        case 62: CDM_ABL(62); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+#undef CDM_ABL
+    return cdm_status();
 }
 
 CDM_API int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx3,

@@ -35,36 +35,7 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-
-
-def preprocess_maps(maps: np.ndarray, size: int = 64) -> torch.Tensor:
-    """code/train_diffusion_condition.py:137-144 (== code/train_diffusion.py:106-113)."""
-    maps = np.asarray(maps, dtype=np.float64)
-    mn = np.min(maps)
-    if mn <= 0:
-        maps = maps - mn + 1e-8
-    maps = maps / np.max(maps)
-    maps = np.log10(maps)
-    maps = (maps - maps.min()) / (maps.max() - maps.min())
-    t = torch.tensor(maps, dtype=torch.float32).unsqueeze(1)
-    return F.interpolate(t, size=(size, size), mode="bilinear")
-
-
-def preprocess_params(params: np.ndarray, n_maps: int, num_params: int, out_dir: str = None):
-    """code/train_diffusion_condition.py:112-134: repeat x15, per-column min-max, select / pad columns."""
-    expanded = np.repeat(params, 15, axis=0)
-    assert expanded.shape[0] == n_maps, "Parameter expansion doesn't match image count"
-    pmin = expanded.min(axis=0, keepdims=True)
-    pmax = expanded.max(axis=0, keepdims=True)
-    norm = (expanded - pmin) / (pmax - pmin + 1e-8)
-    if out_dir:
-        np.save(os.path.join(out_dir, "param_min.npy"), pmin)
-        np.save(os.path.join(out_dir, "param_max.npy"), pmax)
-    if norm.shape[1] > num_params:
-        norm = norm[:, :num_params]
-    elif norm.shape[1] < num_params:
-        norm = np.concatenate([norm, np.zeros((norm.shape[0], num_params - norm.shape[1]))], axis=1)
-    return torch.tensor(norm, dtype=torch.float32)
+from cdm_amd.data import preprocess_maps, preprocess_params, train_test_split  # noqa: E402
 
 
 def main(argv=None):
@@ -115,14 +86,14 @@ def main(argv=None):
         raw_params = torch.rand(max(1, n // 15), 6, generator=g).numpy().astype(np.float64)
         params = preprocess_params(raw_params, n, n_cfeat) if n % 15 == 0 else torch.rand(n, n_cfeat, generator=g)
     else:
-        maps = preprocess_maps(np.load(a.data), H)
+        torch.cuda.set_device(local)
+        maps = preprocess_maps(np.load(a.data, mmap_mode="r"), H)          # device pipeline (csrc/data.hip)
         params = preprocess_params(np.load(a.params), maps.shape[0], n_cfeat, out_dir if rank == 0 else None) \
             if conditional else torch.zeros(maps.shape[0], n_cfeat)
     n_total = maps.shape[0]
     if conditional:
-        test_size = min(1500, n_total // 10)
-        perm = torch.randperm(n_total, generator=torch.Generator().manual_seed(42))
-        test_idx, train_idx = perm[:test_size], perm[test_size:]
+        # random_split(full, [n - 1500, 1500], seed 42) (:150-156); small synthetic sets hold out 10 %
+        train_idx, test_idx = train_test_split(n_total, min(1500, n_total // 10), 42)
     else:
         train_idx, test_idx = torch.arange(n_total), torch.arange(0)
     # data-parallel sharding: every rank sees a disjoint slice of each epoch's permutation

@@ -53,6 +53,10 @@ int cdm_split_bf16x3(const float* b, long long ldb, int K, int N, void* out, voi
 int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
                        const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags, float* stats,
                        int stats_ld, int kc, float* amax_y, void* stream);
+/* timing ablations of the h3 LDS-halo conv (64x64 maps, no bias / stats; tools/conv_ablation.py): abl bits
+ * 1 fragment prefetch, 2 MFMAs doubled, 4 B staged once, 8 halo without the term split (results meaningless) */
+int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int Cin, int ldx, const void* wx,
+                            const float* amax_x, const float* amax_w, float* y, int ldy, int Cout, void* stream);
 int cdm_conv3x3_wgrad_h3(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,
                          const float* amax_dy, const float* amax_x, int splits, float* slab, void* stream);
 /* fp32 [K][N] (ld ldb) -> [ceil(K/16)][3][N][16]: planes 0/1 = fp16 hi/lo of b * 2^(14-e), max|b| = *amax < 2^e */
@@ -71,6 +75,12 @@ int cdm_bin_sum(const double* power, int B, long long NN, const int* off, const 
 /* out[b] = np.histogram(x[b], edges[0..nbins], density=True)[0]  (train_diffusion.py:205-207) */
 int cdm_histogram_density(const float* x, int B, long long P, const double* edges, int nbins, double* out,
                           void* stream);
+/* ---- CAMELS map preprocessing (csrc/data.hip; code/train_diffusion_condition.py:137-144) ----------------------- */
+/* out[0], out[1] = min, max of x[0..n) (keys = 2 unsigned of scratch; order-independent atomics) */
+int cdm_minmax_f32(const float* x, long long n, unsigned* keys, float* out, void* stream);
+/* dst[N][O][O] = bilinear(O x O, align_corners=False)((log10(shift(src) / max) - min) / (max - min)) of src[N][S][S],
+ * with minmax = cdm_minmax_f32 of the whole raw dataset (every step of the reference is monotone) */
+int cdm_camels_maps(const float* src, int N, int S, int O, const float* minmax, float* dst, void* stream);
 /* p[0..n) = 0 (hipMemsetAsync; graph-capturable) */
 int cdm_zero_f32(float* p, long long n, void* stream);
 /* Producers below (cdm_norm_apply_fwd / _bwd, cdm_convT2x2_fwd, cdm_conv3x3_fwd_h3 amax_y) take an optional

@@ -37,3 +37,24 @@ def test_cli_trains_checkpoints_and_samples(tmp_path, args, cond):
         sd = torch.load(out / "weights" / "model_epoch_2.pth", weights_only=True)
         assert len(sd) == 156
         assert np.load(out / "generated_samples.npy").shape == (3, 1, 64, 64)
+
+
+def test_cli_reads_camels_files(tmp_path):
+    """--data / --params: the reference's file formats (maps [N,256,256], params [N/15,6]) through the device
+    preprocessing (cdm_amd.data), the param_min / param_max files and the seeded 90/10 split."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = np.random.default_rng(3)
+    maps = (np.exp(g.normal(size=(30, 256, 256))) * 1e-4).astype(np.float32)
+    params = g.uniform(0.1, 3.0, size=(2, 6))
+    np.save(tmp_path / "maps.npy", maps)
+    np.save(tmp_path / "params.npy", params)
+    out_root = tmp_path / "out"
+    r = subprocess.run([sys.executable, CLI, "1e-3", "1", "20", "6", "--data", str(tmp_path / "maps.npy"),
+                        "--params", str(tmp_path / "params.npy"), "--n-feat", "16", "--batch-size", "8",
+                        "--n-samples", "2", "--out-root", str(out_root)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = out_root / os.listdir(out_root)[0]
+    np.testing.assert_array_equal(np.load(out / "param_min.npy"), params.min(0, keepdims=True))
+    info = open(out / "dataset_info.txt").read()
+    assert "Total dataset size: 30" in info and "Test dataset size: 3" in info
