@@ -7,9 +7,12 @@
         lines 112-134: repeat x15, per-column min-max (param_min.npy / param_max.npy saved), select / pad columns
     train_test_split(n, test_size=1500, seed=42) -> (train_idx, test_idx)
         line 152-156: torch.utils.data.random_split with a seeded generator (the same permutation)
+    params_txt_to_npy(txt, npy) -> array
+        code/txt-npy.py:1-11: whitespace-separated parameter table -> .npy
 
-The maps are processed in the dtype the reference sees for a float32 .npy (fp32).  Large datasets are
-streamed to the device in chunks; the reduction is over the whole dataset, as in the reference.
+The maps are processed in the dtype the reference sees for a float32 .npy (fp32).  The raw maps are uploaded
+once (3.9 GB for the full 15000 x 256^2 set, of 288 GB HBM); the min / max reduction is over the whole dataset,
+as in the reference, and the normalise-and-resize pass runs in chunks of `chunk` maps.
 """
 from __future__ import annotations
 
@@ -69,3 +72,10 @@ def train_test_split(n: int, test_size: int = 1500, seed: int = 42) -> Tuple[tor
     """The index sets of random_split(full, [n - test, test], generator=manual_seed(seed)) (:150-156)."""
     perm = torch.randperm(n, generator=torch.Generator().manual_seed(seed))
     return perm[: n - test_size], perm[n - test_size:]
+
+
+def params_txt_to_npy(txt_path: str, npy_path: str) -> np.ndarray:
+    """code/txt-npy.py:1-11 — np.loadtxt of the whitespace-separated table (float64), saved as .npy."""
+    data = np.loadtxt(txt_path)
+    np.save(npy_path, data)
+    return data

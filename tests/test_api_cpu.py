@@ -66,3 +66,27 @@ def test_cpu_module_fails_loudly():
     m = cdm_amd.ContextUnet(1, 16, 6, 64)
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 1, 64, 64), torch.zeros(1))
+
+
+def test_checkpoint_pth_round_trip(tmp_path, golden_dir):
+    """Checkpoint format (saved as train_diffusion_condition.py:254-255, loaded as
+    sample_power_spectra.py:187-189): torch.save(state_dict) of this model holds the reference's 156 keys in
+    the reference's order, shapes and dtypes, loads with weights_only=True, and a reference-made state_dict
+    (golden, produced by the reference's own ContextUnet) loads into this model unchanged."""
+    import cdm_amd
+    from oracle.ref_cpu import state_dict_layout
+    torch.manual_seed(5)
+    m = cdm_amd.ContextUnet(1, 16, 6, 64)
+    torch.save(m.state_dict(), tmp_path / "model_epoch_99.pth")
+    sd = torch.load(tmp_path / "model_epoch_99.pth", weights_only=True)
+    layout = state_dict_layout(1, 16, 6, 64)
+    assert [k for k, _, _ in layout] == list(sd.keys())
+    for k, shape, _ in layout:
+        assert tuple(sd[k].shape) == shape, k
+        assert sd[k].dtype == (torch.int64 if k.endswith("num_batches_tracked") else torch.float32), k
+    fx = np.load(os.path.join(golden_dir, "model_nf16.npz"))
+    ref = {k[3:]: torch.from_numpy(fx[k].copy()) for k in fx.files if k.startswith("sd.")}
+    m2 = cdm_amd.ContextUnet(1, 16, 6, 64)
+    m2.load_state_dict(ref)
+    for k, v in m2.state_dict().items():
+        assert torch.equal(v, ref[k]), k

@@ -34,3 +34,14 @@ def test_train_test_split_matches_random_split(fx):
     tr, te = data.train_test_split(int(fx["split_n"]), 1500, 42)
     np.testing.assert_array_equal(tr.numpy(), fx["split_train"])
     np.testing.assert_array_equal(te.numpy(), fx["split_test"])
+
+
+def test_params_txt_to_npy_roundtrip(tmp_path):
+    """code/txt-npy.py: the same float64 table as np.loadtxt, written as .npy (CPU host helper)."""
+    import cdm_amd.data as data
+    tab = np.random.default_rng(0).uniform(0.1, 3.0, size=(10, 6))
+    np.savetxt(tmp_path / "param.txt", tab)
+    got = data.params_txt_to_npy(str(tmp_path / "param.txt"), str(tmp_path / "params.npy"))
+    np.testing.assert_array_equal(got, np.loadtxt(tmp_path / "param.txt"))
+    np.testing.assert_array_equal(np.load(tmp_path / "params.npy"), got)
+    assert got.shape == (10, 6) and got.dtype == np.float64
