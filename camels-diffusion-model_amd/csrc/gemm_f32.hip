@@ -1126,6 +1126,169 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
     e(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
 }
 
+// Weight gradient by kernel row: a block owns 128 co x 128 ci x the 3 taps (ky, kx = 0..2) of one kernel row.
+// Per K step (16 pixels of one image row) it stages dY [16 pix][128 co] and the input row segment with its
+// 1-pixel halo X [18 pix][128 ci] once; the 3 taps read B from the same X image at row offsets 0 / 1 / 2 (the
+// kx shift), so each dY fragment feeds 3 taps and X is staged once instead of three times (2.5x less LDS
+// traffic per MFMA than the per-tap kernel above).  8 waves = 2 (co) x 4 (ci), wave tile 64 co x 32 ci x 3
+// taps (6 accumulators).  Split-K over pixel ranges; writes slab[z][co][tap*Cin+ci] like the per-tap kernel.
+template <int NT, int KS = 1>   // KS: 16-pixel K steps per barrier (W % (16 KS) == 0); KS = 2: 1.09x KS = 1
+                                // (KS = 4 needs 133 KB of LDS: the launch is refused)
+__global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __restrict__ dy, int lddy, int Cout,
+                                                              const float* __restrict__ x, int H, int W, int Cin,
+                                                              int ldx, int ktiles, int kt_per_split,
+                                                              const float* amax_dy, const float* amax_x,
+                                                              float* __restrict__ slab) {
+    constexpr int NS = XTerms<NT>::NS;
+    constexpr int RA = 16 * KS, RB = RA + 2;          // image rows (pixels): dY, X with its halo
+    constexpr int IA = RA * 128, IB = RB * 128;       // bf16 per term image
+    constexpr int STEP = NS * (IA + IB);
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STEP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int gx = Cout / 128, T = gx * 3 * (Cin / 128);
+    int L;   // split-major logical order, XCD-contiguous ranges (as the per-tap kernel)
+    {
+        const int nwg = gridDim.x, q8 = nwg >> 3, r8 = nwg & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+        L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + j;
+    }
+    const int bz = L / T, tl = L - bz * T;
+    const int m0 = (tl % gx) * 128, r2 = tl / gx, ky = r2 % 3, ci0 = (r2 / 3) * 128;
+    const int kt0 = bz * kt_per_split, kt1 = min(ktiles, kt0 + kt_per_split);   // in units of KS steps
+    const float sa = op_scale<NT>(amax_dy), sb = op_scale<NT>(amax_x);
+
+    f32x16 acc[3][2];
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][i][r] = 0.f;
+
+    // staging map: thread -> image row sr (pixel), channel quad c4; threads 0..63 also stage X rows 16, 17
+    const int sr = tid >> 5, c4 = (tid & 31) * 4;
+    const int hw = H * W;
+    const int p0 = kt0 * RA;
+    int pn = p0 / hw, ph = (p0 - pn * hw) / W, pw = p0 - pn * hw - ph * W;
+    float4 ra[KS], rb[KS], rb1 = f4zero();
+    auto gload = [&]() {   // the K step at (pn, ph, pw), then advance by RA pixels
+        const int hh = ph + ky - 1;
+        const bool rowok = (unsigned)hh < (unsigned)H;
+        const long long xrow = (long long)(pn * H + hh) * W;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            ra[k] = ld4(dy + ((long long)(pn * H + ph) * W + pw + sr + 16 * k) * lddy + m0 + c4);
+            const int w0 = pw - 1 + sr + 16 * k;
+            rb[k] = (rowok && (unsigned)w0 < (unsigned)W) ? ld4(x + (xrow + w0) * ldx + ci0 + c4) : f4zero();
+        }
+        if (tid < 64) {
+            const int w1 = pw + RA - 1 + sr;
+            rb1 = (rowok && w1 < W) ? ld4(x + (xrow + w1) * ldx + ci0 + c4) : f4zero();
+        }
+        pw += RA;
+        if (pw >= W) { pw = 0; if (++ph == H) { ph = 0; ++pn; } }
+    };
+    auto put = [&](char* img, int row, const float4& v, float sc, int ielems) {
+        const float xv[4] = {v.x, v.y, v.z, v.w};
+        __bf16 h[4], m[4], l[4];
+        split_terms<NT>(xv, sc, h, m, l);
+        char* d = img + trswz(row, c4 >> 3) + (c4 & 7) * 2;
+        *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
+        if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + ielems * 2) = bf16x4{m[0], m[1], m[2], m[3]};
+        if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + ielems * 4) = bf16x4{l[0], l[1], l[2], l[3]};
+    };
+    auto sstore = [&](__bf16* buf) {
+        char* a = reinterpret_cast<char*>(buf);
+        char* b = a + NS * IA * 2;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            put(a, sr + 16 * k, ra[k], sa, IA);
+            put(b, sr + 16 * k, rb[k], sb, IB);
+        }
+        if (tid < 64) put(b, RA + sr, rb1, sb, IB);
+    };
+    // transposed-read addresses (see the per-tap kernel); tap t reads X rows shifted by t
+    const int g = (lane >> 4) & 3, q = (lane >> 2) & 3, pq = lane & 3;
+    const int kb = 8 * (g >> 1) + q;
+    // (the swizzle depends on row & 15 only: K sub-step k adds the constant 16 k rows = 4096 k bytes)
+    int aoff[2][2], boff[3][2];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int ca = wm * 64 + 32 * i + 16 * (g & 1) + 4 * pq;
+            aoff[i][hf] = trswz(kb + 4 * hf, ca >> 3) + (ca & 7) * 2;
+        }
+        const int cb = wn * 32 + 16 * (g & 1) + 4 * pq;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) boff[t][hf] = trswz(kb + 4 * hf + t, cb >> 3) + (cb & 7) * 2;
+    }
+
+    if (kt0 < kt1) { gload(); sstore(smem); }
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) gload();
+        const char* a = reinterpret_cast<const char*>(smem + cur * STEP);
+        const char* b = a + NS * IA * 2;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+        bf16x8 fa[2][NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + s * IA * 2 + aoff[i][0] + 4096 * k));
+                const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + s * IA * 2 + aoff[i][1] + 4096 * k));
+                fa[i][s] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            bf16x8 fb[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const bf16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(b + s * IB * 2 + boff[t][0] + 4096 * k));
+                const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(b + s * IB * 2 + boff[t][1] + 4096 * k));
+                fb[s] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                f32x16 c = acc[t][i];
+                if constexpr (NT >= 6) {
+                    c = xmfma<NT>(fa[i][1], fb[1], c);
+                    c = xmfma<NT>(fa[i][2], fb[0], c);
+                    c = xmfma<NT>(fa[i][0], fb[2], c);
+                }
+                if constexpr (NT >= 3) {
+                    c = xmfma<NT>(fa[i][1], fb[0], c);
+                    c = xmfma<NT>(fa[i][0], fb[1], c);
+                }
+                acc[t][i] = xmfma<NT>(fa[i][0], fb[0], c);
+            }
+        }
+        }
+        if (more) sstore(smem + (cur ^ 1) * STEP);
+        __syncthreads();
+        cur ^= 1;
+    }
+    float ia = 1.f, ib = 1.f;
+    if constexpr (NT == NT_H3) { ia = 1.f / sa; ib = 1.f / sb; }
+    const int NN = 9 * Cin;
+    float* sz = slab + (long long)bz * Cout * NN;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int n = (ky * 3 + t) * Cin + ci0 + wn * 32 + (lane & 31);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                sz[(long long)m * NN + n] = NT == NT_H3 ? (acc[t][i][r] * ia) * ib : acc[t][i][r];
+            }
+    }
+}
+
 template <int WT>
 static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
                             const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm, hipStream_t s) {
@@ -1367,15 +1530,41 @@ CDM_API int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int
                              NT_H3, amax_y, S(stream));
 }
 
+template <int KS>
+static int launch_wgrad_row(const float* dy, int lddy, int Cout, const float* x, int H, int W, int Cin, int ldx, int K,
+                            int sp, const float* amax_dy, const float* amax_x, float* slab, int nterm, hipStream_t st) {
+    const int ktiles = K / (16 * KS), per = (ktiles + sp - 1) / sp;
+    dim3 grid((Cout / 128) * 3 * (Cin / 128) * ((ktiles + per - 1) / per));
+    switch (nterm) {
+        case 1: hipLaunchKernelGGL((wgrad3x3_row_kernel<1, KS>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
+                                   ktiles, per, amax_dy, amax_x, slab); break;
+        case 3: hipLaunchKernelGGL((wgrad3x3_row_kernel<3, KS>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
+                                   ktiles, per, amax_dy, amax_x, slab); break;
+        case NT_H3: hipLaunchKernelGGL((wgrad3x3_row_kernel<NT_H3, KS>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W,
+                                       Cin, ldx, ktiles, per, amax_dy, amax_x, slab); break;
+        case 6: hipLaunchKernelGGL((wgrad3x3_row_kernel<6, KS>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
+                                   ktiles, per, amax_dy, amax_x, slab); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return cdm_status();
+}
+
 // conv3x3 weight gradient on the 16-bit matrix cores (same slab contract as cdm_conv3x3_wgrad); W % 8 == 0
 static int conv3x3_wgrad_split(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,
                                int ldx, const float* amax_dy, const float* amax_x, int splits, float* slab, int nterm,
-                               hipStream_t st) {
+                               hipStream_t st, int variant = 0) {
     if (Cin % 4 || Cout % 4 || W % 8) return (int)hipErrorInvalidValue;
     const int M = Cout, NN = 9 * Cin, K = N * H * W;
     const int sp = effective_splits(K, splits);
     EpiStore ep{slab, NN, (long long)M * NN, nullptr, 1, 0, nullptr, 0, M, NN};
-    if (Cin % 128 == 0 && Cout % 128 == 0 && W % 16 == 0 && lddy % 4 == 0 && ldx % 4 == 0 &&
+    const bool row_ok = Cin % 128 == 0 && Cout % 128 == 0 && lddy % 4 == 0 && ldx % 4 == 0;
+    if ((variant == 0 || variant == 3) && row_ok) {   // kernel-row path (3 taps per block): KS = 2, else 1
+        if (variant == 0 && W % 32 == 0 && effective_splits(K, splits, 32) == sp)
+            return launch_wgrad_row<2>(dy, lddy, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, nterm, st);
+        if (W % 16 == 0 && effective_splits(K, splits, 16) == sp)
+            return launch_wgrad_row<1>(dy, lddy, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, nterm, st);
+    }
+    if (variant != 2 && Cin % 128 == 0 && Cout % 128 == 0 && W % 16 == 0 && lddy % 4 == 0 && ldx % 4 == 0 &&
         effective_splits(K, splits, 16) == sp) {   // transposed-read path
         const int ktiles = K / 16, per = (ktiles + sp - 1) / sp;
         dim3 grid((M / GBM) * (NN / GBN) * ((ktiles + per - 1) / per));
@@ -1408,6 +1597,16 @@ CDM_API int cdm_conv3x3_wgrad_h3(const float* dy, int lddy, int Cout, const floa
                                  void* stream) {
     if (!amax_dy || !amax_x) return (int)hipErrorInvalidValue;
     return conv3x3_wgrad_split(dy, lddy, Cout, x, N, H, W, Cin, ldx, amax_dy, amax_x, splits, slab, NT_H3, S(stream));
+}
+
+// measurement entry: variant 0 = kernel-row kernel, 32-pixel K steps (default path), 1 = per-tap kernel,
+// 2 = generic split GEMM, 3 = kernel-row kernel with 16-pixel K steps
+CDM_API int cdm_conv3x3_wgrad_h3_variant(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W,
+                                         int Cin, int ldx, const float* amax_dy, const float* amax_x, int splits,
+                                         float* slab, int variant, void* stream) {
+    if (!amax_dy || !amax_x || variant < 0 || variant > 3) return (int)hipErrorInvalidValue;
+    return conv3x3_wgrad_split(dy, lddy, Cout, x, N, H, W, Cin, ldx, amax_dy, amax_x, splits, slab, NT_H3, S(stream),
+                               variant);
 }
 
 static int split_blocks(int K, int N) {

@@ -59,6 +59,12 @@ int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int Cin, int 
                             const float* amax_x, const float* amax_w, float* y, int ldy, int Cout, void* stream);
 int cdm_conv3x3_wgrad_h3(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,
                          const float* amax_dy, const float* amax_x, int splits, float* slab, void* stream);
+/* measurement entry of the h3 weight gradient: variant 0 = kernel-row kernel (3 taps per block, 32-pixel K steps,
+ * the default), 1 = per-tap kernel, 2 = generic split GEMM, 3 = kernel-row kernel with 16-pixel K steps; same
+ * slab contract */
+int cdm_conv3x3_wgrad_h3_variant(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,
+                                 int ldx, const float* amax_dy, const float* amax_x, int splits, float* slab,
+                                 int variant, void* stream);
 /* fp32 [K][N] (ld ldb) -> [ceil(K/16)][3][N][16]: planes 0/1 = fp16 hi/lo of b * 2^(14-e), max|b| = *amax < 2^e */
 int cdm_split_f16x2(const float* b, long long ldb, int K, int N, const float* amax, void* out, void* stream);
 /* *out = max(accumulate ? *out : 0, max |x[r*ld + c]|), r < rows, c < C (atomic max, graph-capturable) */
