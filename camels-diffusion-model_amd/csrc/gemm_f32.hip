@@ -148,6 +148,15 @@ struct LdConvT2x2GatherB {  // convT 2x2 wgrad: B(k = input pix (n,h,w), n = ij*
         const int h = rem / W, w = rem - h * W;
         return ld4(dy + ((long long)(n * 2 * H + 2 * h + c.i) * (2 * W) + 2 * w + c.j) * lddy + c.co);
     }
+    // split-bf16 / h3 path: 8 consecutive input pixels k..k+7 (one image row, W % 8 == 0) at one column
+    __device__ __forceinline__ void load8(const Col& c, int k, float (&o)[8]) const {
+        const bool ok = c.ok && k < K;
+        const int hw = H * W; const int n = k / hw; const int rem = k - n * hw;
+        const int h = rem / W, w0 = rem - h * W;
+        const float* p = dy + ((long long)(n * 2 * H + 2 * h + c.i) * (2 * W) + 2 * w0 + c.j) * lddy + c.co;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = ok ? p[(long long)(2 * j) * lddy] : 0.f;
+    }
 };
 
 // ============================== epilogues ==============================
@@ -1394,6 +1403,49 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int splits, i
     }
 }
 
+// the same reduction for N % 4 == 0: a block = 32 float4 columns x 8 split groups; each thread sums every 8th
+// split of its 4 columns with two independent accumulators (memory-level parallelism), the 8 groups are folded
+// through LDS in a fixed order (deterministic).  HBM-bound on the slab read (the scalar kernel above is bound by
+// the latency of its serial split loop).
+__global__ __launch_bounds__(256) void slab_reduce4_kernel(const float* __restrict__ slab, int splits, int M, int N,
+                                                           float* out, long long s_m, long long s_hi, long long s_lo,
+                                                           int csplit, int accumulate, float scale) {
+    __shared__ float4 red[8][32];
+    const long long total4 = (long long)M * N / 4;
+    const int col = threadIdx.x & 31, zg = threadIdx.x >> 5;
+    const long long i4 = (long long)blockIdx.x * 32 + col;
+    float4 a0 = f4zero(), a1 = f4zero();
+    if (i4 < total4) {
+        const float4* p = reinterpret_cast<const float4*>(slab) + i4;
+        int z = zg;
+        for (; z + 8 < splits; z += 16) {
+            const float4 u = p[(long long)z * total4], v = p[(long long)(z + 8) * total4];
+            a0.x += u.x; a0.y += u.y; a0.z += u.z; a0.w += u.w;
+            a1.x += v.x; a1.y += v.y; a1.z += v.z; a1.w += v.w;
+        }
+        if (z < splits) {
+            const float4 u = p[(long long)z * total4];
+            a0.x += u.x; a0.y += u.y; a0.z += u.z; a0.w += u.w;
+        }
+    }
+    red[zg][col] = make_float4(a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w);
+    __syncthreads();
+    if (zg == 0 && i4 < total4) {
+        float4 v = red[0][col];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) { const float4 u = red[k][col]; v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w; }
+        const float vv[4] = {v.x * scale, v.y * scale, v.z * scale, v.w * scale};
+        const long long idx = i4 * 4;
+        const int m = (int)(idx / N), n0 = (int)(idx - (long long)m * N);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int n = n0 + e, hi = n / csplit, lo = n - hi * csplit;
+            float* q = out + m * s_m + hi * s_hi + lo * s_lo;
+            *q = accumulate ? *q + vv[e] : vv[e];
+        }
+    }
+}
+
 }  // namespace cdm
 
 using namespace cdm;
@@ -1681,6 +1733,33 @@ CDM_API int cdm_convT2x2_dgrad(const float* dy, int N, int H, int W, int Cout, i
     return launch_gemm<LdConvT2x2GatherA, LdDenseB, EpiStore, false>(la, lb, ep, M, Cin, K, 1, S(stream));
 }
 
+// h3 ConvT 2x2 dgrad: A = gathered dY (k = (ij, co), max|dY| = *amax_dy), B = cdm_split_f16x2 of the packed
+// wpkT [4 Cout][Cin] with max|W| = *amax_w
+CDM_API int cdm_convT2x2_dgrad_h3(const float* dy, int N, int H, int W, int Cout, int lddy, const void* wx,
+                                  const float* amax_dy, const float* amax_w, float* dx, int lddx, int Cin, int flags,
+                                  void* stream) {
+    if (Cin % 4 || Cout % 4 || !amax_dy || !amax_w) return (int)hipErrorInvalidValue;
+    const int M = N * H * W, K = 4 * Cout;
+    EpiStore ep{dx, lddx, 0, nullptr, 1, flags, nullptr, 0, M, Cin};
+    return launch_gemm_x3<RowK<LdConvT2x2GatherA>::template T, StagePre, EpiStore, true>(
+        MkRowK<LdConvT2x2GatherA>{LdConvT2x2GatherA{dy, H, W, Cout, lddy, M, K}, amax_dy},
+        MkPre{reinterpret_cast<const __bf16*>(wx), Cin, amax_w}, ep, M, Cin, K, 1, NT_H3, S(stream));
+}
+
+// h3 ConvT 2x2 weight gradient (same slab contract as cdm_convT2x2_wgrad); W % 8 == 0
+CDM_API int cdm_convT2x2_wgrad_h3(const float* x, int N, int H, int W, int Cin, int ldx, const float* dy, int Cout,
+                                  int lddy, const float* amax_x, const float* amax_dy, int splits, float* slab,
+                                  void* stream) {
+    if (Cin % 4 || Cout % 4 || W % 8 || !amax_x || !amax_dy) return (int)hipErrorInvalidValue;
+    const int M = Cin, NN = 4 * Cout, K = N * H * W;
+    const int sp = effective_splits(K, splits);
+    EpiStore ep{slab, NN, (long long)M * NN, nullptr, 1, 0, nullptr, 0, M, NN};
+    return launch_gemm_x3<ColK<LdDenseAT>::template T, ColK<LdConvT2x2GatherB>::template T, EpiStore, false>(
+        MkColK<LdDenseAT>{LdDenseAT{x, ldx, M, K}, amax_x},
+        MkColK<LdConvT2x2GatherB>{LdConvT2x2GatherB{dy, H, W, Cout, lddy, K, NN}, amax_dy}, ep, M, NN, K, sp, NT_H3,
+        S(stream));
+}
+
 // C[m][n] = A[m][k] . B[k][n] (+bias[n % bias_mod]).  splits > 1: writes raw partials to slab[z][M][N].
 CDM_API int cdm_gemm_f32(const float* a, long long lda, int M, int K, const float* b, long long ldb, int N,
                          float* c, long long ldc, const float* bias, int bias_mod, int flags, int splits,
@@ -1737,6 +1816,12 @@ CDM_API int cdm_gemm_tn_f32(const float* a, long long lda, int M, int K, const f
 CDM_API int cdm_slab_reduce(const float* slab, int splits, int M, int N, float* out, long long s_m, long long s_hi,
                             long long s_lo, int csplit, int accumulate, float scale, void* stream) {
     const long long total = (long long)M * N;
+    if (N % 4 == 0 && splits >= 8) {
+        const long long blocks4 = (total / 4 + 31) / 32;
+        hipLaunchKernelGGL(slab_reduce4_kernel, dim3((unsigned)blocks4), dim3(256), 0, S(stream), slab, splits, M, N, out,
+                           s_m, s_hi, s_lo, csplit > 0 ? csplit : N, accumulate, scale);
+        return cdm_status();
+    }
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;

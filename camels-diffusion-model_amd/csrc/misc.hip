@@ -843,6 +843,11 @@ CDM_API int cdm_transpose(const float* in, int R, int C, float* out, void* strea
     transpose_tiled(in, 1, R, C, out, S(stream));
     return cdm_status();
 }
+/* in [batch][R][C] -> out [batch][C][R] */
+CDM_API int cdm_transpose_batched(const float* in, int batch, int R, int C, float* out, void* stream) {
+    transpose_tiled(in, batch, R, C, out, S(stream));
+    return cdm_status();
+}
 __global__ void counter_add_kernel(int* c, int d) { if (threadIdx.x == 0) *c += d; }
 CDM_API int cdm_counter_add(int* ctr, int delta, void* stream) {
     hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, S(stream), ctr, delta);

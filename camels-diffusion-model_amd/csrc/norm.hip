@@ -172,18 +172,29 @@ __global__ __launch_bounds__(256) void slab_colsum_kernel(const float* __restric
 // -------------------------------------------------------------------------------------------------
 // BatchNorm (train): per channel over all ntiles = N*nchunks partials.  Updates running stats like
 // torch (momentum 0.1, unbiased running var), increments num_batches_tracked (int64) once.
-__global__ void bn_fwd_finalize_kernel(const double* part, int S, int R, int C, double count,
+// Block = 16 channels x 16 lanes over the S partials (strided), folded through LDS in a fixed order.
+__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* part, int S, int R, int C, double count,
                                        const float* gamma, const float* beta, float* rmean, float* rvar,
                                        long long* nbt, float momentum, float eps, float* mean, float* invstd,
                                        float* scale, float* shift) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c == 0 && nbt) *nbt += 1;
-    if (c >= C) return;
-    double s = 0.0, q = 0.0;
-    for (int t = 0; t < S; ++t) {
-        s += part[((long long)t * R + 0) * C + c];
-        q += part[((long long)t * R + 1) * C + c];
+    __shared__ double rs[16][17], rq[16][17];
+    const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
+    const int c = blockIdx.x * 16 + cl;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+    {
+        double s = 0.0, q = 0.0;
+        if (c < C)
+            for (int t = ln; t < S; t += 16) {
+                s += part[((long long)t * R + 0) * C + c];
+                q += part[((long long)t * R + 1) * C + c];
+            }
+        rs[ln][cl] = s; rq[ln][cl] = q;
     }
+    __syncthreads();
+    if (ln != 0 || c >= C) return;
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { s += rs[k][cl]; q += rq[k][cl]; }
     const double mu = s / count;
     double var = q / count - mu * mu;
     if (var < 0.0) var = 0.0;
@@ -238,16 +249,26 @@ __global__ void gn_fwd_finalize_kernel(const float* slab, int nchunks, int R, in
 }
 
 // BatchNorm backward: dgamma/dbeta (assign), dy = A*gpre + B + Cc*xhat coefficients, conv bias grad.
-__global__ void bn_bwd_finalize_kernel(const double* part, int S, int C, double count, const float* gamma,
-                                       const float* invstd, float* dgamma, float* dbeta, float* A, float* B,
-                                       float* Cc, float* dbias) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s1 = 0.0, s2 = 0.0, s5 = 0.0;
-    for (int t = 0; t < S; ++t) {
-        const double* p = part + (long long)t * 5 * C;
-        s1 += p[0 * C + c]; s2 += p[1 * C + c]; s5 += p[4 * C + c];
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* part, int S, int C, double count,
+                                       const float* gamma, const float* invstd, float* dgamma, float* dbeta, float* A,
+                                       float* B, float* Cc, float* dbias) {
+    __shared__ double r1[16][17], r2[16][17], r5[16][17];
+    const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
+    const int c = blockIdx.x * 16 + cl;
+    {
+        double s1 = 0.0, s2 = 0.0, s5 = 0.0;
+        if (c < C)
+            for (int t = ln; t < S; t += 16) {
+                const double* p = part + (long long)t * 5 * C;
+                s1 += p[0 * C + c]; s2 += p[1 * C + c]; s5 += p[4 * C + c];
+            }
+        r1[ln][cl] = s1; r2[ln][cl] = s2; r5[ln][cl] = s5;
     }
+    __syncthreads();
+    if (ln != 0 || c >= C) return;
+    double s1 = 0.0, s2 = 0.0, s5 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { s1 += r1[k][cl]; s2 += r2[k][cl]; s5 += r5[k][cl]; }
     const double a = (double)gamma[c] * (double)invstd[c];
     const double b = -a * s1 / count, cc = -a * s2 / count;
     dgamma[c] = (float)s2; dbeta[c] = (float)s1;
@@ -472,7 +493,7 @@ CDM_API int cdm_slab_colsum(const float* slab, int ntiles, int R, int C, double*
 CDM_API int cdm_bn_fwd_finalize(const double* part, int nparts, int R, int C, double count, const float* gamma,
                                 const float* beta, float* rmean, float* rvar, long long* nbt, float momentum, float eps,
                                 float* mean, float* invstd, float* scale, float* shift, void* stream) {
-    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), part, nparts, R, C, count,
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, S(stream), part, nparts, R, C, count,
                        gamma, beta, rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift);
     return cdm_status();
 }
@@ -496,7 +517,7 @@ CDM_API int cdm_gn_fwd_finalize(const float* slab, int N, int nchunks, int R, in
 CDM_API int cdm_bn_bwd_finalize(const double* part, int nparts, int C, double count, const float* gamma,
                                 const float* invstd, float* dgamma, float* dbeta, float* A, float* B, float* Cc,
                                 float* dbias, void* stream) {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), part, nparts, C, count,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, S(stream), part, nparts, C, count,
                        gamma, invstd, dgamma, dbeta, A, B, Cc, dbias);
     return cdm_status();
 }

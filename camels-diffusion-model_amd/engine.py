@@ -171,6 +171,8 @@ class UNetEngine:
             self.pk[name + ".wt"], self.pk[name + ".wtT"] = wt, wtT
             if self.nterm == NT_H3:
                 self._split(name + ".wt", cin, 4 * nf, stream)
+                if train:
+                    self._split(name + ".wtT", 4 * nf, cin, stream)
         c0 = 2 * nf
         w0 = self._buf("up0.wt", (c0, self.KK0 * c0))
         w0T = self._buf("up0.wtT", (self.KK0 * c0, c0))
@@ -474,7 +476,10 @@ class UNetEngine:
         KN = self.KK0 * c0
         sp = lb.raw("cdm_gemm_splits")(B, 1)
         lb.cdm_gemm_tn_f32(_p(ws.hv), c0, c0, B, _p(ws.D2), KN, KN, 1, _p(ws.slab), s)
-        lb.cdm_slab_reduce(_p(ws.slab), sp, c0, KN, _p(G["up0.0.weight"]), KN, 1, self.KK0, c0, 0, 1.0, s)
+        if sp == 1:   # [ci][ij][co] -> [ci][co][ij]: a batched tiled transpose
+            lb.cdm_transpose_batched(_p(ws.slab), c0, self.KK0, c0, _p(G["up0.0.weight"]), s)
+        else:
+            lb.cdm_slab_reduce(_p(ws.slab), sp, c0, KN, _p(G["up0.0.weight"]), KN, 1, self.KK0, c0, 0, 1.0, s)
         # dhv[n][ci] = sum_{(ij,co)} dy0[n][(ij,co)] W[ci][co][ij]   (split-K over 16*16*2nf)
         want = max(1, min(64, _cdiv(1024, _cdiv(B, 128) * _cdiv(c0, 128))))
         sp = lb.raw("cdm_gemm_splits")(KN, want)
@@ -543,8 +548,12 @@ class UNetEngine:
             return
         self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s, amax_dy=dslot, amax_x=self._src_slot(ws, l))
         dgd = ws.dgrad_dst[l.name]
+        gslot = self._slot(ws, "gT:" + l.name) if l.name in self._CONVT_GRAD_PRODUCERS else None
         self.conv3x3(l.name + ".wdg", dy.p, B, S, C, dy.ld, None, dgd.p, dgd.ld, l.cin,
-                     EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s, amax_x=dslot)
+                     EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s, amax_x=dslot, amax_y=gslot)
+
+    # the dgrads that write the gradient wrt a ConvT output (gT1 / gT2) also record its max for the h3 ConvT bwd
+    _CONVT_GRAD_PRODUCERS = {"up1.model.1.conv1": "up1.model.0", "up2.model.1.conv1": "up2.model.0"}
 
     def _wgrad3x3(self, ws, dy: Act, x: Act, B, S, cin, cout, gW, s, amax_dy=None, amax_x=None):
         lb = lib()
@@ -573,10 +582,21 @@ class UNetEngine:
         nparts = fold(ws, _p(ws.slab), B * _cdiv(Ho * Ho, CHUNK), 1, cout, s)
         lb.cdm_slab_sum_all(_p(ws.dpart), nparts, 1, 0, 1, cout, _p(G[name + ".bias"]), 0, 1, 0, s)
         sp = wgrad_splits(B * Hin * Hin, cin, 4 * cout)
-        lb.cdm_convT2x2_wgrad(x.p, B, Hin, Hin, cin, x.ld, gy.p, cout, gy.ld, sp, _p(ws.slab), s)
+        h3 = self.nterm == NT_H3
+        if h3:
+            prod = next(k for k, v in self._CONVT_GRAD_PRODUCERS.items() if v == name)
+            a_gy = self._slot(ws, "gT:" + prod)
+            a_x = self._slot(ws, {"up1.model.0": "catU1", "up2.model.0": "catU2"}[name])
+            lb.cdm_convT2x2_wgrad_h3(x.p, B, Hin, Hin, cin, x.ld, gy.p, cout, gy.ld, a_x, a_gy, sp, _p(ws.slab), s)
+        else:
+            lb.cdm_convT2x2_wgrad(x.p, B, Hin, Hin, cin, x.ld, gy.p, cout, gy.ld, sp, _p(ws.slab), s)
         # slab[z][ci][ij*cout+co] -> [ci][co][ij]
         lb.cdm_slab_reduce(_p(ws.slab), sp, cin, 4 * cout, _p(G[name + ".weight"]), 4 * cout, 1, 4, cout, 0, 1.0, s)
-        lb.cdm_convT2x2_dgrad(gy.p, B, Hin, Hin, cout, gy.ld, _p(self.pk[name + ".wtT"]), dx.p, dx.ld, cin, 0, s)
+        if h3:
+            lb.cdm_convT2x2_dgrad_h3(gy.p, B, Hin, Hin, cout, gy.ld, _p(self.pk[name + ".wtT_x"]), a_gy,
+                                     _p(self.pk[name + ".wtT_amax"]), dx.p, dx.ld, cin, 0, s)
+        else:
+            lb.cdm_convT2x2_dgrad(gy.p, B, Hin, Hin, cout, gy.ld, _p(self.pk[name + ".wtT"]), dx.p, dx.ld, cin, 0, s)
 
     def _gn_bwd(self, ws, P, name, bias_name, g: Act, mode, y: Act, B, S, C, st, film_a, film_an, dy: Act, G, s,
                 film_out=None, amax=None):

@@ -112,6 +112,13 @@ int cdm_conv3x3_wgrad(const float* dy, int lddy, int Cout, const float* x, int N
                       int splits, float* slab, void* stream);
 int cdm_convT2x2_wgrad(const float* x, int N, int H, int W, int Cin, int ldx, const float* dy, int Cout, int lddy,
                        int splits, float* slab, void* stream);
+/* h3 variants of the ConvT 2x2 backward: dgrad with wx = cdm_split_f16x2 of wpkT [4 Cout][Cin] (max|W| = *amax_w)
+ * and max|dy| = *amax_dy; wgrad with max|x| = *amax_x, max|dy| = *amax_dy (W % 8 == 0).  Same semantics. */
+int cdm_convT2x2_dgrad_h3(const float* dy, int N, int H, int W, int Cout, int lddy, const void* wx,
+                          const float* amax_dy, const float* amax_w, float* dx, int lddx, int Cin, int flags,
+                          void* stream);
+int cdm_convT2x2_wgrad_h3(const float* x, int N, int H, int W, int Cin, int ldx, const float* dy, int Cout, int lddy,
+                          const float* amax_x, const float* amax_dy, int splits, float* slab, void* stream);
 int cdm_gemm_tn_f32(const float* a, long long lda, int M, int K, const float* b, long long ldb, int N, int splits,
                     float* slab, void* stream);
 /* out[m*s_m + (n/csplit)*s_hi + (n%csplit)*s_lo] (+)= scale * sum_z slab[z][m][n] */
@@ -217,6 +224,8 @@ int cdm_pack_conv3x3(const float* W, const float* b, int Cin, int Cout, const fl
                      void* stream);
 int cdm_pack_convT(const float* W, int Cin, int Cout, int KK, float* wt, float* wtT, void* stream);
 int cdm_transpose(const float* in, int R, int C, float* out, void* stream);
+/* batched: in [batch][R][C] -> out [batch][C][R] (64x64 LDS tiles) */
+int cdm_transpose_batched(const float* in, int batch, int R, int C, float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -145,6 +145,22 @@ def test_convT2x2(L, N, Hin, Cin, Cout):
     L.cdm_slab_reduce(slab.data_ptr(), sp, Cin, 4 * Cout, dW.data_ptr(), 4 * Cout, 1, 4, Cout, 0, 1.0, _s())
     torch.cuda.synchronize()
     _close(dW, Wg.grad, 5e-5)
+    # h3 backward (engine default): dgrad from the pre-split wpkT, wgrad with both operands scaled + split
+    amg = _amax(L, gyn, N * 4 * Hin * Hin, Cout)
+    wxT, amwT = _split_h3(L, wtT, 4 * Cout, Cin)
+    dx3 = torch.empty_like(dx)
+    L.cdm_convT2x2_dgrad_h3(gyn.data_ptr(), N, Hin, Hin, Cout, Cout, wxT.data_ptr(), amg.data_ptr(), amwT.data_ptr(),
+                            dx3.data_ptr(), Cin, Cin, 0, _s())
+    torch.cuda.synchronize()
+    _close(_nchw(dx3, N, Hin, Hin, Cin), xg.grad)
+    if Hin % 8 == 0:
+        slab.fill_(float("nan"))
+        L.cdm_convT2x2_wgrad_h3(xn.data_ptr(), N, Hin, Hin, Cin, Cin, gyn.data_ptr(), Cout, Cout, amx.data_ptr(),
+                                amg.data_ptr(), sp, slab.data_ptr(), _s())
+        dW3 = torch.empty_like(dW)
+        L.cdm_slab_reduce(slab.data_ptr(), sp, Cin, 4 * Cout, dW3.data_ptr(), 4 * Cout, 1, 4, Cout, 0, 1.0, _s())
+        torch.cuda.synchronize()
+        _close(dW3, Wg.grad, 5e-5)
 
 
 @pytest.mark.parametrize("M,K,N,splits", [(5, 256, 4096, 1), (256, 256, 8192, 1), (10, 4096, 64, 16), (130, 36, 132, 1)])
