@@ -62,6 +62,20 @@ class _Lib:
 
     @staticmethod
     def _checked(name, fn):
+        if os.environ.get("CDM_TRACE_CALLS") == "1":   # debugging: name every call, synchronise after it
+            import sys
+            import torch
+
+            def traced(*args):
+                print("[cdm]", name, args, file=sys.stderr, flush=True)
+                rc = fn(*args)
+                torch.cuda.synchronize()
+                if rc != 0:
+                    raise HipError(f"{name} failed with hipError_t {rc}")
+                return rc
+            traced.__name__ = name
+            return traced
+
         def call(*args):
             rc = fn(*args)
             if rc != 0:

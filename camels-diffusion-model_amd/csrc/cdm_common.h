@@ -56,3 +56,13 @@ static __device__ __forceinline__ void block_amax_commit(float m, float* out) {
         atomicMax(reinterpret_cast<unsigned*>(out), __float_as_uint(m));
     }
 }
+
+// BatchNorm (+ReLU) backward of one element.  norm_apply_bwd_kernel and the fused conv staging
+// (gemm_f32.hip, PreBnBwd) both use this one expression, so the fused and unfused paths produce
+// bit-identical dy:   z_pre = y s + t,  xhat = (y - mean) invstd,  dy = A (z_pre > 0 ? g : 0) + B + Cc xhat
+static __device__ __forceinline__ float bn_bwd_elem(float g, float y, float s, float t, float mean, float invstd,
+                                                    float a, float b, float cc) {
+    const float zp = fmaf(y, s, t);
+    const float xh = (y - mean) * invstd;
+    return fmaf(cc, xh, fmaf(a, zp > 0.f ? g : 0.f, b));
+}

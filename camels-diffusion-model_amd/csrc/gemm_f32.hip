@@ -718,6 +718,16 @@ struct MkPre {
 template <class LD> struct RowK { template <int NT> using T = StageRowK<LD, NT>; };
 template <class LD> struct ColK { template <int NT> using T = StageColK<LD, NT>; };
 
+// Optional staging pre-op of a conv operand.  PreBnBwd: the operand is dy of a Conv -> BatchNorm -> ReLU layer,
+// computed while staging from the grad g of the ReLU output and the pre-norm activations y (bn_bwd_elem, the
+// expression of norm_apply_bwd_kernel): dy is never written to HBM (no 537 MB write + 2 reads per layer).
+struct PreNone { static constexpr bool on = false; };
+struct PreBnBwd {
+    static constexpr bool on = true;
+    const float* y; int ldy;   // pre-norm activations [pix][C]
+    const float* p[7];         // per channel: scale s, shift t, mean, invstd, A, B, Cc
+};
+
 // ============================== LDS-halo conv3x3 on the split-bf16 matrix cores ==============================
 // conv3x3 (stride 1, pad 1) forward / dgrad for Cin % 16 == 0 (channel-chunk-major K, kc = 16) and image
 // width WT in {32, 64}.  A block owns 256 consecutive output pixels (= 256/WT whole image rows) x 128
@@ -737,11 +747,11 @@ constexpr int HTHREADS = 512;
 // tap's fragments are read during the current tap's MFMAs: 0.94 -> 0.84 ms), 2 every MFMA issued twice, 4 B
 // staged once (stale afterwards), 8 halo stored without the term split, 16 no barriers in the main loop,
 // 32 halo loaded for the first chunk only
-template <int NT, int WT, class EP, bool XCD_REMAP, int ABL = (NT >= 6 ? 0 : 1)>
+template <int NT, int WT, class EP, bool XCD_REMAP, int ABL = (NT >= 6 ? 0 : 1), class PRE = PreNone>
 __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const float* __restrict__ x, int H, int Cin,
                                                                       int ldx, const __bf16* __restrict__ wx3,
                                                                       int Cout, const float* amax_x,
-                                                                      const float* amax_w, EP ep) {
+                                                                      const float* amax_w, EP ep, PRE pre) {
     constexpr int NS = XTerms<NT>::NS;
     constexpr int ROWS = HBM_ / WT, HR = ROWS + 2, HC = WT + 2, HPX = HR * HC;
     constexpr int HPLANE = HPX * XBK;                 // bf16 per halo term plane
@@ -763,6 +773,15 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     const int hw = H * WT, img = m0 / hw, h0 = (m0 - img * hw) / WT;
     const int nchunks = Cin / 16, ngroups = nchunks * 3;
     const float sx = op_scale<NT>(amax_x);
+    // BN-backward pre-op: the block's per-channel coefficients, staged once (Cin <= 256)
+    __shared__ __attribute__((aligned(16))) float bcs[PRE::on ? 7 * 256 : 4];
+    if constexpr (PRE::on) {
+        for (int i = tid; i < 7 * Cin; i += HTHREADS) {
+            const int k = i / Cin;
+            bcs[i] = pre.p[k][i - k * Cin];
+        }
+        __syncthreads();
+    }
 
     f32x16 acc[2][2];
 #pragma unroll
@@ -776,14 +795,17 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     float4 hreg[HQ];
     const float* hsrc[HQ];          // chunk-0 source of piece j (nullptr: zero padding / past the halo)
     int hdst[HQ];                   // its LDS offset within a term plane
+    float4 yreg[PRE::on ? HQ : 1];  // PreBnBwd: the pre-norm activations of piece j
+    const float* hysrc[PRE::on ? HQ : 1];
 #pragma unroll
     for (int j = 0; j < HQ; ++j) {
         const int q = tid + j * HTHREADS;
         const int hp = q >> 2, c4 = q & 3;
         const int hr = hp / HC, hc = hp - hr * HC;
         const int ih = h0 - 1 + hr, iw = hc - 1;
-        hsrc[j] = (q < HPX * 4 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)WT)
-                      ? x + ((long long)(img * H + ih) * WT + iw) * ldx + c4 * 4 : nullptr;
+        const bool in = q < HPX * 4 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)WT;
+        hsrc[j] = in ? x + ((long long)(img * H + ih) * WT + iw) * ldx + c4 * 4 : nullptr;
+        if constexpr (PRE::on) hysrc[j] = in ? pre.y + ((long long)(img * H + ih) * WT + iw) * pre.ldy + c4 * 4 : nullptr;
         hdst[j] = q < HPX * 4 ? xoff(hp, c4 * 4) : -1;
     }
     auto gload_halo = [&](int cc) {
@@ -791,13 +813,33 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
             if (cc > 0) return;
         }
 #pragma unroll
-        for (int j = 0; j < HQ; ++j) hreg[j] = hsrc[j] ? ld4(hsrc[j] + cc * 16) : f4zero();
+        for (int j = 0; j < HQ; ++j) {
+            hreg[j] = hsrc[j] ? ld4(hsrc[j] + cc * 16) : f4zero();
+            if constexpr (PRE::on) yreg[j] = hysrc[j] ? ld4(hysrc[j] + cc * 16) : f4zero();
+        }
     };
-    auto store_halo = [&](__bf16* base) {
+    auto store_halo = [&](__bf16* base, int cc) {
+        float cf[PRE::on ? 7 : 1][4];   // coefficients of this thread's 4 channels (q & 3 == tid & 3 for every j)
+        if constexpr (PRE::on) {
+            const int cb = cc * 16 + (tid & 3) * 4;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                const float4 v = *reinterpret_cast<const float4*>(bcs + k * Cin + cb);
+                cf[k][0] = v.x; cf[k][1] = v.y; cf[k][2] = v.z; cf[k][3] = v.w;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < HQ; ++j) {
             if (hdst[j] >= 0) {
-                const float xv[4] = {hreg[j].x, hreg[j].y, hreg[j].z, hreg[j].w};
+                float xv[4] = {hreg[j].x, hreg[j].y, hreg[j].z, hreg[j].w};
+                if constexpr (PRE::on) {
+                    if (hsrc[j]) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            xv[e] = bn_bwd_elem(xv[e], f4get(yreg[j], e), cf[0][e], cf[1][e], cf[2][e], cf[3][e],
+                                                cf[4][e], cf[5][e], cf[6][e]);
+                    }
+                }
                 __bf16 h[4], m[4], l[4];
                 if constexpr (ABL & 8) {
 #pragma unroll
@@ -941,7 +983,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     };
     gload_halo(0);
     gload_b(0, bregA);
-    store_halo(Hs);
+    store_halo(Hs, 0);
     store_b(Bs, bregA);
     __syncthreads();
     int hb = 0, bb = 0;
@@ -965,7 +1007,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         // dy = 2: fetch B of the next chunk's dy = 0; split + store the next halo (buffer idle since chunk cc-1)
         // ahead of this group's MFMAs, so its VALU work interleaves with them; B after them (just issued)
         if (morec) gload_b(g0 + 3, bregA);
-        if (morec) store_halo(Hs + (hb ^ 1) * NS * HPLANE);
+        if (morec) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
         compute(2, a, Bs + bb * BPL * XPLANE);
         if (morec) store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregA);
         sync();
@@ -1141,13 +1183,14 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
 // kx shift), so each dY fragment feeds 3 taps and X is staged once instead of three times (2.5x less LDS
 // traffic per MFMA than the per-tap kernel above).  8 waves = 2 (co) x 4 (ci), wave tile 64 co x 32 ci x 3
 // taps (6 accumulators).  Split-K over pixel ranges; writes slab[z][co][tap*Cin+ci] like the per-tap kernel.
-template <int NT, int KS = 1>   // KS: 16-pixel K steps per barrier (W % (16 KS) == 0); KS = 2: 1.09x KS = 1
-                                // (KS = 4 needs 133 KB of LDS: the launch is refused)
+template <int NT, int KS = 1, class PRE = PreNone>   // KS: 16-pixel K steps per barrier (W % (16 KS) == 0);
+                                // KS = 2: 1.09x KS = 1 (KS = 4 needs 133 KB of LDS: the launch is refused)
+                                // PRE = PreBnBwd: dy computed from g (the dy argument) and y while staging
 __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __restrict__ dy, int lddy, int Cout,
                                                               const float* __restrict__ x, int H, int W, int Cin,
                                                               int ldx, int ktiles, int kt_per_split,
                                                               const float* amax_dy, const float* amax_x,
-                                                              float* __restrict__ slab) {
+                                                              float* __restrict__ slab, PRE pre) {
     constexpr int NS = XTerms<NT>::NS;
     constexpr int RA = 16 * KS, RB = RA + 2;          // image rows (pixels): dY, X with its halo
     constexpr int IA = RA * 128, IB = RB * 128;       // bf16 per term image
@@ -1180,13 +1223,24 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
     const int p0 = kt0 * RA;
     int pn = p0 / hw, ph = (p0 - pn * hw) / W, pw = p0 - pn * hw - ph * W;
     float4 ra[KS], rb[KS], rb1 = f4zero();
+    float4 ya[PRE::on ? KS : 1];
+    float cf[PRE::on ? 7 : 1][4];   // PreBnBwd coefficients of this thread's 4 output channels m0 + c4
+    if constexpr (PRE::on) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const float4 v = ld4(pre.p[k] + m0 + c4);
+            cf[k][0] = v.x; cf[k][1] = v.y; cf[k][2] = v.z; cf[k][3] = v.w;
+        }
+    }
     auto gload = [&]() {   // the K step at (pn, ph, pw), then advance by RA pixels
         const int hh = ph + ky - 1;
         const bool rowok = (unsigned)hh < (unsigned)H;
         const long long xrow = (long long)(pn * H + hh) * W;
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
-            ra[k] = ld4(dy + ((long long)(pn * H + ph) * W + pw + sr + 16 * k) * lddy + m0 + c4);
+            const long long pix = (long long)(pn * H + ph) * W + pw + sr + 16 * k;
+            ra[k] = ld4(dy + pix * lddy + m0 + c4);
+            if constexpr (PRE::on) ya[k] = ld4(pre.y + pix * pre.ldy + m0 + c4);
             const int w0 = pw - 1 + sr + 16 * k;
             rb[k] = (rowok && (unsigned)w0 < (unsigned)W) ? ld4(x + (xrow + w0) * ldx + ci0 + c4) : f4zero();
         }
@@ -1211,7 +1265,17 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
         char* b = a + NS * IA * 2;
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
-            put(a, sr + 16 * k, ra[k], sa, IA);
+            if constexpr (PRE::on) {
+                const float yv[4] = {ya[k].x, ya[k].y, ya[k].z, ya[k].w};
+                float gv[4] = {ra[k].x, ra[k].y, ra[k].z, ra[k].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    gv[e] = bn_bwd_elem(gv[e], yv[e], cf[0][e], cf[1][e], cf[2][e], cf[3][e], cf[4][e], cf[5][e],
+                                        cf[6][e]);
+                put(a, sr + 16 * k, make_float4(gv[0], gv[1], gv[2], gv[3]), sa, IA);
+            } else {
+                put(a, sr + 16 * k, ra[k], sa, IA);
+            }
             put(b, sr + 16 * k, rb[k], sb, IB);
         }
         if (tid < 64) put(b, RA + sr, rb1, sb, IB);
@@ -1298,20 +1362,21 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
     }
 }
 
-template <int WT>
+template <int WT, class PRE = PreNone>
 static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
-                            const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm, hipStream_t s) {
+                            const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm, hipStream_t s,
+                            PRE pre = PRE{}) {
     const int M = N * H * WT;
     dim3 grid(M / HBM_, (Cout + GBN - 1) / GBN, 1);
     switch (nterm) {
-        case 1: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep); break;
-        case 3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<3, WT, EpiStoreW<4>, true>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep); break;
-        case NT_H3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EpiStoreW<4>, true>), grid, dim3(HTHREADS), 0,
-                                       s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep); break;
-        case 6: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<6, WT, EpiStoreW<4>, true>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep); break;
+        case 1: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, (1 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre); break;
+        case 3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<3, WT, EpiStoreW<4>, true, (3 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre); break;
+        case NT_H3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EpiStoreW<4>, true, (NT_H3 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0,
+                                       s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre); break;
+        case 6: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<6, WT, EpiStoreW<4>, true, (6 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre); break;
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();
@@ -1545,7 +1610,7 @@ CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int C
     dim3 grid(M / HBM_, (Cout + GBN - 1) / GBN, 1);
     hipStream_t s = S(stream);
 #define CDM_ABL(A) hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, 64, EpiStoreW<4>, true, A>), grid, dim3(HTHREADS), 0, \
-                                      s, x, H, Cin, ldx, b, Cout, amax_x, amax_w, eh)
+                                      s, x, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, PreNone{})
     switch (abl) {
         case 0: CDM_ABL(0); break;
         case 1: CDM_ABL(1); break;
@@ -1566,6 +1631,26 @@ CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int C
     return cdm_status();
 }
 
+// conv3x3 dgrad of a Conv -> BatchNorm -> ReLU layer with the BN backward fused into the halo staging: the conv
+// input dy = bn_bwd_elem(g, y, coefficients) is computed per staged element (dy never materialised).  C = BN
+// channels (the dgrad's input channels), Cout = the dgrad's output channels.  W == H in {32, 64}, C % 16 == 0,
+// C <= 256; wx = cdm_split_f16x2 of the kc = 16 packed dgrad weights; max|dy| <= *amax_dy (cdm_bn_bwd_amax_bound).
+CDM_API int cdm_conv3x3_dgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
+                                       const float* t, const float* mean, const float* invstd, const float* A,
+                                       const float* B, const float* Cc, int N, int H, int W, int C, const void* wx,
+                                       const float* amax_dy, const float* amax_w, float* out, int ldo, int Cout,
+                                       int flags, float* amax_out, void* stream) {
+    if (W != H || (W != 64 && W != 32) || C % 16 || C > 256 || ldg % 4 || ldy % 4 || (H * W) % HBM_ ||
+        !amax_dy || !amax_w)
+        return (int)hipErrorInvalidValue;
+    const int M = N * H * W;
+    const EpiStoreW<4> eh{out, ldo, 0, nullptr, Cout, flags, nullptr, 0, M, Cout, amax_out};
+    const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
+    const __bf16* b = reinterpret_cast<const __bf16*>(wx);
+    return W == 64 ? launch_conv_halo<64>(g, N, H, C, ldg, b, Cout, amax_dy, amax_w, eh, NT_H3, S(stream), pre)
+                   : launch_conv_halo<32>(g, N, H, C, ldg, b, Cout, amax_dy, amax_w, eh, NT_H3, S(stream), pre);
+}
+
 CDM_API int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx3,
                                const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
                                int kc, int nterm, void* stream) {
@@ -1582,20 +1667,21 @@ CDM_API int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int
                              NT_H3, amax_y, S(stream));
 }
 
-template <int KS>
+template <int KS, class PRE = PreNone>
 static int launch_wgrad_row(const float* dy, int lddy, int Cout, const float* x, int H, int W, int Cin, int ldx, int K,
-                            int sp, const float* amax_dy, const float* amax_x, float* slab, int nterm, hipStream_t st) {
+                            int sp, const float* amax_dy, const float* amax_x, float* slab, int nterm, hipStream_t st,
+                            PRE pre = PRE{}) {
     const int ktiles = K / (16 * KS), per = (ktiles + sp - 1) / sp;
     dim3 grid((Cout / 128) * 3 * (Cin / 128) * ((ktiles + per - 1) / per));
     switch (nterm) {
-        case 1: hipLaunchKernelGGL((wgrad3x3_row_kernel<1, KS>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
-                                   ktiles, per, amax_dy, amax_x, slab); break;
-        case 3: hipLaunchKernelGGL((wgrad3x3_row_kernel<3, KS>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
-                                   ktiles, per, amax_dy, amax_x, slab); break;
-        case NT_H3: hipLaunchKernelGGL((wgrad3x3_row_kernel<NT_H3, KS>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W,
-                                       Cin, ldx, ktiles, per, amax_dy, amax_x, slab); break;
-        case 6: hipLaunchKernelGGL((wgrad3x3_row_kernel<6, KS>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
-                                   ktiles, per, amax_dy, amax_x, slab); break;
+        case 1: hipLaunchKernelGGL((wgrad3x3_row_kernel<1, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
+                                   ktiles, per, amax_dy, amax_x, slab, pre); break;
+        case 3: hipLaunchKernelGGL((wgrad3x3_row_kernel<3, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
+                                   ktiles, per, amax_dy, amax_x, slab, pre); break;
+        case NT_H3: hipLaunchKernelGGL((wgrad3x3_row_kernel<NT_H3, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W,
+                                       Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre); break;
+        case 6: hipLaunchKernelGGL((wgrad3x3_row_kernel<6, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
+                                   ktiles, per, amax_dy, amax_x, slab, pre); break;
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();
@@ -1659,6 +1745,24 @@ CDM_API int cdm_conv3x3_wgrad_h3_variant(const float* dy, int lddy, int Cout, co
     if (!amax_dy || !amax_x || variant < 0 || variant > 3) return (int)hipErrorInvalidValue;
     return conv3x3_wgrad_split(dy, lddy, Cout, x, N, H, W, Cin, ldx, amax_dy, amax_x, splits, slab, NT_H3, S(stream),
                                variant);
+}
+
+// conv3x3 weight gradient of a Conv -> BatchNorm -> ReLU layer with the BN backward fused into the dY staging of
+// the kernel-row kernel (same slab contract as cdm_conv3x3_wgrad_h3).  Cin % 128 == Cout % 128 == 0, W % 16 == 0.
+CDM_API int cdm_conv3x3_wgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
+                                       const float* t, const float* mean, const float* invstd, const float* A,
+                                       const float* B, const float* Cc, int Cout, const float* x, int N, int H, int W,
+                                       int Cin, int ldx, const float* amax_dy, const float* amax_x, int splits,
+                                       float* slab, void* stream) {
+    if (Cin % 128 || Cout % 128 || W % 16 || ldg % 4 || ldy % 4 || ldx % 4 || !amax_dy || !amax_x)
+        return (int)hipErrorInvalidValue;
+    const int K = N * H * W, sp = effective_splits(K, splits);
+    const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
+    if (W % 32 == 0 && effective_splits(K, splits, 32) == sp)
+        return launch_wgrad_row<2>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, NT_H3, S(stream), pre);
+    if (effective_splits(K, splits, 16) == sp)
+        return launch_wgrad_row<1>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, NT_H3, S(stream), pre);
+    return (int)hipErrorInvalidValue;
 }
 
 static int split_blocks(int K, int N) {

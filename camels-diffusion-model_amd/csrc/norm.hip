@@ -48,7 +48,7 @@ struct SumF {  // R=1: plain sum (bias gradients)
 
 // Recompute one element's forward pieces.
 static __device__ __forceinline__ void norm_elem(const NormP& np, int n, int c, float y, float& zpre, float& xhat) {
-    zpre = y * np.s[n * np.sn + c] + np.t[n * np.sn + c];
+    zpre = fmaf(y, np.s[n * np.sn + c], np.t[n * np.sn + c]);
     const int gi = n * np.mn + c / np.cpg;
     xhat = (y - np.mean[gi]) * np.invstd[gi];
 }
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(256) void norm_apply_bwd_kernel(const float* g, int
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const float gpre = (e == arg && zp[e] > 0.f) ? f4get(gv, j) : 0.f;
-                    out[e][j] = a * gpre + b + cc * xh[e];
+                    out[e][j] = fmaf(cc, xh[e], fmaf(a, gpre, b));
                 }
             }
 #pragma unroll
@@ -433,11 +433,11 @@ __global__ __launch_bounds__(256) void norm_apply_bwd_kernel(const float* g, int
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int c = c4 + j;
-                float zp, xh; norm_elem(np, n, c, f4get(yv, j), zp, xh);
+                const int si = n * np.sn + c, gi = n * np.mn + c / np.cpg;
                 float gz = f4get(gv, j);
                 if constexpr (FILM) gz *= fp.a[n * fp.an + c];
-                const float gpre = zp > 0.f ? gz : 0.f;
-                out[j] = A[n * cn + c] * gpre + B[n * cn + c] + Cc[n * cn + c] * xh;
+                out[j] = bn_bwd_elem(gz, f4get(yv, j), np.s[si], np.t[si], np.mean[gi], np.invstd[gi], A[n * cn + c],
+                                     B[n * cn + c], Cc[n * cn + c]);
             }
             st4(dy + pix * lddy + c4, make_float4(out[0], out[1], out[2], out[3]));
 #pragma unroll
@@ -445,6 +445,18 @@ __global__ __launch_bounds__(256) void norm_apply_bwd_kernel(const float* g, int
         }
     }
     if (amax) block_amax_commit(am, amax);
+}
+
+// upper bound of max|dy| for the fused BN backward (dy never materialised): per channel
+// |A| max|g| + |B| + |Cc| (max|y| + |mean|) invstd >= |A g_pre + B + Cc xhat|; max over channels into *out
+__global__ __launch_bounds__(256) void bn_bwd_amax_bound_kernel(int C, const float* A, const float* B, const float* Cc,
+                                                                const float* mean, const float* invstd,
+                                                                const float* amax_g, const float* amax_y, float* out) {
+    const float G = *amax_g, Y = *amax_y;
+    float m = 0.f;
+    for (int c = threadIdx.x; c < C; c += blockDim.x)
+        m = fmaxf(m, fabsf(A[c]) * G + fabsf(B[c]) + fabsf(Cc[c]) * (Y + fabsf(mean[c])) * invstd[c]);
+    block_amax_commit(m, out);
 }
 
 static inline int ew_blocks(long long total) {
@@ -589,5 +601,14 @@ CDM_API int cdm_norm_apply_bwd(int mode, const float* g, int ldg, const float* y
     else
         hipLaunchKernelGGL((norm_apply_bwd_kernel<false, false>), dim3(nb), dim3(256), 0, S(stream), g, ldg, y, ldy, N, H,
                            W, C, np, fp, A, B, Cc, cn, dy, lddy, amax);
+    return cdm_status();
+}
+
+CDM_API int cdm_bn_bwd_amax_bound(int C, const float* A, const float* B, const float* Cc, const float* mean,
+                                  const float* invstd, const float* amax_g, const float* amax_y, float* amax_dy,
+                                  void* stream) {
+    if (!amax_g || !amax_y || !amax_dy) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_bwd_amax_bound_kernel, dim3(1), dim3(256), 0, S(stream), C, A, B, Cc, mean, invstd, amax_g,
+                       amax_y, amax_dy);
     return cdm_status();
 }

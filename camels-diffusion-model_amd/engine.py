@@ -24,6 +24,7 @@ x-hat from y.  Eval mode folds BatchNorm into the conv weights and runs ReLU in 
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional
 
 import torch
@@ -114,6 +115,9 @@ class UNetEngine:
         self.nf, self.ncf, self.H = n_feat, n_cfeat, height
         self.conv_math = conv_math
         self.nterm = CONV_MATH[conv_math]
+        # h3 train: BatchNorm backward fused into the staging of the layer's dgrad / wgrad (dy never written);
+        # $CDM_FUSE_BN_BWD=0 keeps the separate apply kernel (A/B checks)
+        self.fuse_bn_bwd = self.nterm == NT_H3 and os.environ.get("CDM_FUSE_BN_BWD", "1") != "0"
         self.device = torch.device(device)
         self.layers = conv_layers(n_feat, height)
         self.L = {l.name: l for l in self.layers}
@@ -231,6 +235,11 @@ class UNetEngine:
         else:
             lib().cdm_conv3x3_fwd(x_p, B, S, S, cin, ldx, _p(self.pk[key]), bias_p, y_p, ldy, cout, flags, stats_p,
                                   stats_ld, kc, s)
+
+    def fuses_bn_bwd(self, l: "LayerSpec", kind: str) -> bool:
+        """Layer l's BN backward runs inside its dgrad / wgrad staging (cdm_conv3x3_*_h3_bnbwd)."""
+        return (self.fuse_bn_bwd and kind == "dense" and l.cin > 1 and l.S in (32, 64) and l.kc == 16
+                and l.cin % 128 == 0 and l.cout % 128 == 0 and l.cout <= 256)
 
     # h3 operand maxima: one device slot per producer, zeroed at the start of every forward --------------
     def _slot(self, ws, key):
@@ -361,8 +370,9 @@ class UNetEngine:
                 lb.cdm_reduce_stats(_p(y), l.cout, B, S * S, l.cout, CHUNK, _p(ws.slab), s)
                 ntiles = B * _cdiv(S * S, CHUNK)
             else:
+                yslot = self._slot(ws, "y:" + l.name) if l.name in ws.fused else None
                 self.conv3x3(l.name + ".wpk", src.p, B, S, l.cin, src.ld, _p(P[l.b]), _p(y), l.cout, l.cout, 0,
-                             _p(ws.slab), l.cout, l.kc, s, amax_x=self._src_slot(ws, l))
+                             _p(ws.slab), l.cout, l.kc, s, amax_x=self._src_slot(ws, l), amax_y=yslot)
                 ntiles = _cdiv(npix, CHUNK)
             bn = l.bn
             nparts = fold(ws, _p(ws.slab), ntiles, 2, l.cout, s)
@@ -535,6 +545,25 @@ class UNetEngine:
         lb.cdm_bn_bwd_finalize(_p(ws.dpart), nparts, C, float(B * S * S), _p(P[bn + ".weight"]), _p(st["invstd"]),
                                _p(G[bn + ".weight"]), _p(G[bn + ".bias"]), _p(co[0]), _p(co[1]), _p(co[2]),
                                _p(G[l.b]), s)
+        gslot = self._dgrad_amax_slot(ws, l)
+        if l.name in ws.fused:
+            # dy = bn_bwd(g, y) inside the staging of both convs; its scale from a bound on max|dy|
+            dslot = self._slot(ws, "dy:" + l.name)
+            lb.cdm_bn_bwd_amax_bound(C, _p(co[0]), _p(co[1]), _p(co[2]), _p(st["mean"]), _p(st["invstd"]),
+                                     self._slot(ws, "g:" + l.name), self._slot(ws, "y:" + l.name), dslot, s)
+            coef = (_p(st["scale"]), _p(st["shift"]), _p(st["mean"]), _p(st["invstd"]), _p(co[0]), _p(co[1]),
+                    _p(co[2]))
+            src = ws.src[l.name]
+            sp = wgrad_splits(B * S * S, C, 9 * l.cin)
+            lb.cdm_conv3x3_wgrad_h3_bnbwd(g.p, g.ld, _p(y), C, *coef, C, src.p, B, S, S, l.cin, src.ld, dslot,
+                                          self._src_slot(ws, l), sp, _p(ws.slab), s)
+            lb.cdm_slab_reduce(_p(ws.slab), sp, C, 9 * l.cin, _p(G[l.w]), 9 * l.cin, 1, 9, l.cin, 0, 1.0, s)
+            dgd = ws.dgrad_dst[l.name]
+            key = l.name + ".wdg"
+            lb.cdm_conv3x3_dgrad_h3_bnbwd(g.p, g.ld, _p(y), C, *coef, B, S, S, C, _p(self.pk[key + "_x"]), dslot,
+                                          _p(self.pk[key + "_amax"]), dgd.p, dgd.ld, l.cin,
+                                          EPI_ACCUM if ws.dgrad_accum[l.name] else 0, gslot, s)
+            return
         dy = ws.dy[l.name]
         dslot = self._slot(ws, "dy:" + l.name) if l.cin > 1 else None
         lb.cdm_norm_apply_bwd(mode, g.p, g.ld, _p(y), C, B, S, S, C, _p(st["scale"]), _p(st["shift"]), 0,
@@ -548,9 +577,16 @@ class UNetEngine:
             return
         self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s, amax_dy=dslot, amax_x=self._src_slot(ws, l))
         dgd = ws.dgrad_dst[l.name]
-        gslot = self._slot(ws, "gT:" + l.name) if l.name in self._CONVT_GRAD_PRODUCERS else None
         self.conv3x3(l.name + ".wdg", dy.p, B, S, C, dy.ld, None, dgd.p, dgd.ld, l.cin,
                      EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s, amax_x=dslot, amax_y=gslot)
+
+    def _dgrad_amax_slot(self, ws, l: "LayerSpec"):
+        """Slot that receives max|dgrad output| of layer l: the grad wrt a ConvT output (h3 ConvT backward) or
+        the grad g of a fused layer (its dy bound)."""
+        if l.name in self._CONVT_GRAD_PRODUCERS:
+            return self._slot(ws, "gT:" + l.name)
+        key = ws.g_amax_key.get(l.name)
+        return self._slot(ws, key) if key else None
 
     # the dgrads that write the gradient wrt a ConvT output (gT1 / gT2) also record its max for the h3 ConvT bwd
     _CONVT_GRAD_PRODUCERS = {"up1.model.1.conv1": "up1.model.0", "up2.model.1.conv1": "up2.model.0"}
@@ -728,7 +764,7 @@ class Workspace:
             else:
                 self.src[l.name] = self.dst[prev[l.name]]
         self.slab = E(self._slab_floats())
-        self.amax = torch.zeros(96, device=dev)   # h3 operand maxima, one slot per producer (UNetEngine._slot)
+        self.amax = torch.zeros(192, device=dev)  # h3 operand maxima, one slot per producer (UNetEngine._slot)
         self.aslot = {}
         self.dpart = torch.empty(10 * 32768 + 4096, device=dev, dtype=torch.float64)
         self.sc_pending = None
@@ -771,6 +807,41 @@ class Workspace:
                     self.dgrad_dst[l.name], self.dgrad_accum[l.name] = Act(Gb, l.cin), False
                 elif l.cin > 1:
                     self.dgrad_dst[l.name], self.dgrad_accum[l.name] = Act(Gb, l.cin), False
+            self._wire_fused_bn_bwd(eng, L, kinds)
+        else:
+            self.fused, self.g_amax_key = set(), {}
+
+    def _wire_fused_bn_bwd(self, eng, L, kinds):
+        """Fused layers read g and write their dgrad without a dy buffer in between, so g and the dgrad output
+        must differ: walking the backward order, each fused layer writes its dgrad into the other buffer of its
+        resolution's pair (G, D), which becomes the g of the layer before it.  Non-fused layers keep dy in D
+        (in place when their g already sits in D: the mode-0 apply is elementwise, index for index)."""
+        self.fused = {l.name for l in L if eng.fuses_bn_bwd(l, kinds[l.name])}
+        self.g_amax_key = {}
+        if not self.fused:
+            return
+        other = {}
+        for a_, b_ in ((self.G0, self.D0), (self.G1, self.D1)):
+            other[a_.data_ptr()], other[b_.data_ptr()] = b_, a_
+        idx = {l.name: i for i, l in enumerate(L)}
+        for l in reversed(L):
+            if l.name not in self.fused:
+                continue
+            nxt = L[idx[l.name] + 1]                      # its g is written by the next layer's dgrad
+            self.g_amax_key[nxt.name] = "g:" + l.name
+            g = self.gout[l.name]
+            if l.name in ("down1.model.0.conv1", "down2.model.0.conv1"):
+                continue                                  # dgrad accumulates into a concat-grad slice
+            dst = other[g.buf.data_ptr()]
+            self.dgrad_dst[l.name] = Act(dst, l.cin)
+            if l.name == "up1.model.1.conv1":
+                self.gT1 = dst
+            elif l.name == "up2.model.1.conv1":
+                self.gT2 = dst
+            else:
+                prev = L[idx[l.name] - 1]
+                assert kinds[prev.name] == "dense", prev.name
+                self.gout[prev.name] = Act(dst, prev.cout)
 
     def _slab_floats(self):
         eng, B = self.eng, self.B
@@ -782,6 +853,8 @@ class Workspace:
                 if l.cin > 1:
                     sp = wgrad_splits(B * l.S * l.S, l.cout, 9 * l.cin)
                     need = max(need, sp * l.cout * 9 * l.cin)
+            # out.0 (2nf -> nf at full resolution; not in eng.layers)
+            need = max(need, wgrad_splits(P0, nf, 9 * 2 * nf) * nf * 9 * 2 * nf)
             for cin, Hin in ((4 * nf, H // 4), (2 * nf, H // 2)):   # convT wgrad
                 need = max(need, wgrad_splits(B * Hin * Hin, cin, 4 * nf) * cin * 4 * nf)
             need = max(need, 2 * nf * eng.KK0 * 2 * nf)     # up0 weight grad

@@ -65,6 +65,20 @@ int cdm_conv3x3_wgrad_h3(const float* dy, int lddy, int Cout, const float* x, in
 int cdm_conv3x3_wgrad_h3_variant(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,
                                  int ldx, const float* amax_dy, const float* amax_x, int splits, float* slab,
                                  int variant, void* stream);
+/* Conv -> BatchNorm -> ReLU backward with the BN backward fused into the conv staging (dy never written):
+ * dy = A (y s + t > 0 ? g : 0) + B + Cc (y - mean) invstd per element (the expression of cdm_norm_apply_bwd
+ * mode 0, bit-identical), s/t/mean/invstd/A/B/Cc per channel.  dgrad: LDS-halo kernel, W == H in {32, 64},
+ * C % 16 == 0, C <= 256, C = BN channels, Cout = dgrad output channels, wx = split packed dgrad weights;
+ * wgrad: kernel-row kernel (Cin, Cout % 128 == 0, W % 16 == 0), same slab contract as cdm_conv3x3_wgrad_h3.
+ * max|dy| <= *amax_dy from cdm_bn_bwd_amax_bound. */
+int cdm_conv3x3_dgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
+                               const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
+                               int N, int H, int W, int C, const void* wx, const float* amax_dy, const float* amax_w,
+                               float* out, int ldo, int Cout, int flags, float* amax_out, void* stream);
+int cdm_conv3x3_wgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
+                               const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
+                               int Cout, const float* x, int N, int H, int W, int Cin, int ldx, const float* amax_dy,
+                               const float* amax_x, int splits, float* slab, void* stream);
 /* fp32 [K][N] (ld ldb) -> [ceil(K/16)][3][N][16]: planes 0/1 = fp16 hi/lo of b * 2^(14-e), max|b| = *amax < 2^e */
 int cdm_split_f16x2(const float* b, long long ldb, int K, int N, const float* amax, void* out, void* stream);
 /* *out = max(accumulate ? *out : 0, max |x[r*ld + c]|), r < rows, c < C (atomic max, graph-capturable) */
@@ -162,6 +176,10 @@ int cdm_norm_apply_bwd(int mode, const float* g, int ldg, const float* y, int ld
                        const float* s, const float* t, int sn, const float* mean, const float* invstd, int mn, int cpg,
                        const float* film_a, int film_an, const float* A, const float* B, const float* Cc, int cn,
                        float* dy, int lddy, float* amax, void* stream);
+/* *amax_dy = max(*amax_dy, max_c |A| max|g| + |B| + |Cc| (max|y| + |mean|) invstd): an upper bound of max|dy| of
+ * the fused BN backward (from the producers' max|g| = *amax_g and max|y| = *amax_y); one block */
+int cdm_bn_bwd_amax_bound(int C, const float* A, const float* B, const float* Cc, const float* mean,
+                          const float* invstd, const float* amax_g, const float* amax_y, float* amax_dy, void* stream);
 
 /* ---- small ops (csrc/misc.hip) ---------------------------------------------------------------- */
 /* init_conv.conv1: Conv2d(1, nf, 3, 1, 1) (ContextUnet.py:14 -> diffusion_utilities.py:27) */

@@ -352,3 +352,57 @@ def test_split_f16x2_terms(L):
     wd = w.double()
     bound = torch.maximum(2.0 ** -22 * wd.abs(), torch.full_like(wd, 2.0 ** (e - 14 - 25)))
     assert ((rec - wd).abs() <= bound).all()
+
+
+@pytest.mark.parametrize("N,S,C,Cin", [(2, 64, 128, 128), (2, 32, 256, 128), (1, 32, 128, 256), (2, 32, 256, 256)])
+def test_bn_bwd_fused_into_conv_staging_bit_exact(L, N, S, C, Cin):
+    """Fused BN backward (dy computed while staging, never written) == norm_apply_bwd mode 0 then the h3
+    convs, bit for bit: dgrad (LDS-halo kernel) and wgrad (kernel-row kernel) at the same operand scale; the
+    scale comes from cdm_bn_bwd_amax_bound, which must bound max|dy|."""
+    from cdm_amd.engine import wgrad_splits
+    g_ = torch.Generator(device="cuda").manual_seed(5)
+    P = N * S * S
+    gr = torch.randn(P, C, device="cuda", generator=g_) * 1e-3
+    y = torch.randn(P, C, device="cuda", generator=g_) * 2 + 0.3
+    x = torch.randn(P, Cin, device="cuda", generator=g_).relu()
+    co = [torch.randn(C, device="cuda", generator=g_) for _ in range(7)]
+    co[3] = co[3].abs() + 0.1                                   # invstd > 0
+    s_, t_, mean, invstd, A, B, Cc = co
+    dy = torch.empty(P, C, device="cuda")
+    am = torch.zeros(4, device="cuda")                          # [max|dy| exact, bound, max|g|, max|y|]
+    L.cdm_norm_apply_bwd(0, gr.data_ptr(), C, y.data_ptr(), C, N, S, S, C, s_.data_ptr(), t_.data_ptr(), 0,
+                         mean.data_ptr(), invstd.data_ptr(), 0, 1, None, 0, A.data_ptr(), B.data_ptr(), Cc.data_ptr(),
+                         0, dy.data_ptr(), C, am.data_ptr(), _s())
+    L.cdm_amax_f32(gr.data_ptr(), P, C, C, am.data_ptr() + 8, 0, _s())
+    L.cdm_amax_f32(y.data_ptr(), P, C, C, am.data_ptr() + 12, 0, _s())
+    L.cdm_bn_bwd_amax_bound(C, A.data_ptr(), B.data_ptr(), Cc.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                            am.data_ptr() + 8, am.data_ptr() + 12, am.data_ptr() + 4, _s())
+    torch.cuda.synchronize()
+    assert am[1].item() >= am[0].item() > 0
+    dslot = am.data_ptr() + 4
+    coefs = [t.data_ptr() for t in co]
+    # dgrad: weights [Cin][C][3][3] as the dgrad of a conv C -> ... (dgrad maps C channels to Cin)
+    W = torch.randn(C, Cin, 3, 3) * 0.05
+    wdg = torch.empty(9 * C, Cin, device="cuda")
+    L.cdm_pack_conv3x3(W.cuda().data_ptr(), torch.zeros(C, device="cuda").data_ptr(), Cin, C, None, None, None, None,
+                       0.0, torch.empty(9 * Cin, C, device="cuda").data_ptr(), None, wdg.data_ptr(), 16, _s())
+    wx, amw = _split_h3(L, wdg, 9 * C, Cin)
+    ref = torch.empty(P, Cin, device="cuda"); got = torch.empty(P, Cin, device="cuda")
+    a1 = torch.zeros(2, device="cuda")
+    L.cdm_conv3x3_fwd_h3(dy.data_ptr(), N, S, S, C, C, wx.data_ptr(), dslot, amw.data_ptr(), None, ref.data_ptr(), Cin,
+                         Cin, 0, None, 0, 16, a1.data_ptr(), _s())
+    L.cdm_conv3x3_dgrad_h3_bnbwd(gr.data_ptr(), C, y.data_ptr(), C, *coefs, N, S, S, C, wx.data_ptr(), dslot,
+                                 amw.data_ptr(), got.data_ptr(), Cin, Cin, 0, a1.data_ptr() + 4, _s())
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert a1[0].item() == a1[1].item() == ref.abs().max().item()
+    # wgrad of the conv Cin -> C that produced y: dW[co=C][tap*Cin+ci]
+    amx = _amax(L, x, P, Cin)
+    sp = wgrad_splits(P, C, 9 * Cin)
+    s_ref = torch.empty(sp, C, 9 * Cin, device="cuda"); s_got = torch.full_like(s_ref, float("nan"))
+    L.cdm_conv3x3_wgrad_h3(dy.data_ptr(), C, C, x.data_ptr(), N, S, S, Cin, Cin, dslot, amx.data_ptr(), sp,
+                           s_ref.data_ptr(), _s())
+    L.cdm_conv3x3_wgrad_h3_bnbwd(gr.data_ptr(), C, y.data_ptr(), C, *coefs, C, x.data_ptr(), N, S, S, Cin, Cin, dslot,
+                                 amx.data_ptr(), sp, s_got.data_ptr(), _s())
+    torch.cuda.synchronize()
+    assert torch.equal(s_got, s_ref)
