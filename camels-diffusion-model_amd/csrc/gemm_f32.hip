@@ -730,7 +730,7 @@ struct PreBnBwd {
 
 // ============================== LDS-halo conv3x3 on the split-bf16 matrix cores ==============================
 // conv3x3 (stride 1, pad 1) forward / dgrad for Cin % 16 == 0 (channel-chunk-major K, kc = 16) and image
-// width WT in {32, 64}.  A block owns 256 consecutive output pixels (= 256/WT whole image rows) x 128
+// width WT in {32, 64} (128, 256 with the two-term h3 arithmetic).  A block owns 256 consecutive output pixels (= 256/WT whole image rows) x 128
 // output channels, 8 waves as 4 (M) x 2 (N), each wave 64x64.  Per 16-channel chunk the block stages its
 // input rows plus the 1-pixel halo ((256/WT + 2) x (WT + 2) pixels x 16 ch) ONCE into LDS, split into
 // bf16 terms, and the 9 taps of that chunk read their A fragments straight out of the halo tile at
@@ -1368,6 +1368,14 @@ static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, cons
                             PRE pre = PRE{}) {
     const int M = N * H * WT;
     dim3 grid(M / HBM_, (Cout + GBN - 1) / GBN, 1);
+    if constexpr (WT > 64) {
+        // wide rows (C5: 128 / 256 columns): a block is 256 / WT whole rows, halo (256/WT + 2) x (WT + 2);
+        // LDS fits the two-term (h3) image only (WT 256: 2 x 2 x 774 px x 32 B + 48 KiB B = 145 KiB)
+        if (nterm != NT_H3) return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EpiStoreW<4>, true, 1, PRE>), grid, dim3(HTHREADS), 0, s,
+                           x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre);
+        return cdm_status();
+    } else {
     switch (nterm) {
         case 1: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, (1 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
                                    Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre); break;
@@ -1380,6 +1388,26 @@ static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, cons
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();
+    }
+}
+
+// LDS-halo conv of a W x W image (W in {32, 64}; 128 / 256 with the h3 arithmetic only)
+template <class PRE = PreNone>
+static int launch_conv_halo_w(int W, const float* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
+                              const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm,
+                              hipStream_t s, PRE pre = PRE{}) {
+    switch (W) {
+        case 32: return launch_conv_halo<32>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
+        case 64: return launch_conv_halo<64>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
+        case 128: return launch_conv_halo<128>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
+        case 256:   // the BN-backward staging registers do not fit next to the 7 halo pieces of a 256-wide row
+            if constexpr (PRE::on) return (int)hipErrorInvalidValue;
+            else return launch_conv_halo<256>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+static bool halo_width_ok(int W, int nterm) {
+    return W == 32 || W == 64 || ((W == 128 || W == 256) && nterm == NT_H3);
 }
 
 // b [K][N] fp32 (ld ldb)  ->  out [ceil(K/16)][3][N][16] bf16 split terms (k >= K zero-filled)
@@ -1578,11 +1606,10 @@ static int conv3x3_fwd_split(const float* x, int N, int H, int W, int Cin, int l
     const int M = N * H * W, K = 9 * Cin;
     MkPre mb{reinterpret_cast<const __bf16*>(wx), Cout, amax_w};
     EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
-    if (kc == 16 && W == H && (W == 64 || W == 32) && ldx % 4 == 0 && (H * W) % HBM_ == 0) {   // LDS-halo path
+    if (kc == 16 && W == H && halo_width_ok(W, nterm) && ldx % 4 == 0 && (H * W) % HBM_ == 0) {   // LDS-halo path
         const EpiStoreW<4> eh{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
         const __bf16* b = reinterpret_cast<const __bf16*>(wx);
-        return W == 64 ? launch_conv_halo<64>(x, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st)
-                       : launch_conv_halo<32>(x, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st);
+        return launch_conv_halo_w(W, x, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st);
     }
     if (Cin == 128 && Cout == 128 && H == 64 && W == 64 && kc == 16) {
         using LA = LdIm2colA<128, 16, 64>;
@@ -1633,22 +1660,21 @@ CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int C
 
 // conv3x3 dgrad of a Conv -> BatchNorm -> ReLU layer with the BN backward fused into the halo staging: the conv
 // input dy = bn_bwd_elem(g, y, coefficients) is computed per staged element (dy never materialised).  C = BN
-// channels (the dgrad's input channels), Cout = the dgrad's output channels.  W == H in {32, 64}, C % 16 == 0,
+// channels (the dgrad's input channels), Cout = the dgrad's output channels.  W == H in {32, 64, 128}, C % 16 == 0,
 // C <= 256; wx = cdm_split_f16x2 of the kc = 16 packed dgrad weights; max|dy| <= *amax_dy (cdm_bn_bwd_amax_bound).
 CDM_API int cdm_conv3x3_dgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
                                        const float* t, const float* mean, const float* invstd, const float* A,
                                        const float* B, const float* Cc, int N, int H, int W, int C, const void* wx,
                                        const float* amax_dy, const float* amax_w, float* out, int ldo, int Cout,
                                        int flags, float* amax_out, void* stream) {
-    if (W != H || (W != 64 && W != 32) || C % 16 || C > 256 || ldg % 4 || ldy % 4 || (H * W) % HBM_ ||
+    if (W != H || !halo_width_ok(W, NT_H3) || W > 128 || C % 16 || C > 256 || ldg % 4 || ldy % 4 || (H * W) % HBM_ ||
         !amax_dy || !amax_w)
         return (int)hipErrorInvalidValue;
     const int M = N * H * W;
     const EpiStoreW<4> eh{out, ldo, 0, nullptr, Cout, flags, nullptr, 0, M, Cout, amax_out};
     const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
     const __bf16* b = reinterpret_cast<const __bf16*>(wx);
-    return W == 64 ? launch_conv_halo<64>(g, N, H, C, ldg, b, Cout, amax_dy, amax_w, eh, NT_H3, S(stream), pre)
-                   : launch_conv_halo<32>(g, N, H, C, ldg, b, Cout, amax_dy, amax_w, eh, NT_H3, S(stream), pre);
+    return launch_conv_halo_w(W, g, N, H, C, ldg, b, Cout, amax_dy, amax_w, eh, NT_H3, S(stream), pre);
 }
 
 CDM_API int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx3,

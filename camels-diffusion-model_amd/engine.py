@@ -238,7 +238,7 @@ class UNetEngine:
 
     def fuses_bn_bwd(self, l: "LayerSpec", kind: str) -> bool:
         """Layer l's BN backward runs inside its dgrad / wgrad staging (cdm_conv3x3_*_h3_bnbwd)."""
-        return (self.fuse_bn_bwd and kind == "dense" and l.cin > 1 and l.S in (32, 64) and l.kc == 16
+        return (self.fuse_bn_bwd and kind == "dense" and l.cin > 1 and l.S in (32, 64, 128) and l.kc == 16
                 and l.cin % 128 == 0 and l.cout % 128 == 0 and l.cout <= 256)
 
     # h3 operand maxima: one device slot per producer, zeroed at the start of every forward --------------

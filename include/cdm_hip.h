@@ -67,7 +67,7 @@ int cdm_conv3x3_wgrad_h3_variant(const float* dy, int lddy, int Cout, const floa
                                  int variant, void* stream);
 /* Conv -> BatchNorm -> ReLU backward with the BN backward fused into the conv staging (dy never written):
  * dy = A (y s + t > 0 ? g : 0) + B + Cc (y - mean) invstd per element (the expression of cdm_norm_apply_bwd
- * mode 0, bit-identical), s/t/mean/invstd/A/B/Cc per channel.  dgrad: LDS-halo kernel, W == H in {32, 64},
+ * mode 0, bit-identical), s/t/mean/invstd/A/B/Cc per channel.  dgrad: LDS-halo kernel, W == H in {32, 64, 128},
  * C % 16 == 0, C <= 256, C = BN channels, Cout = dgrad output channels, wx = split packed dgrad weights;
  * wgrad: kernel-row kernel (Cin, Cout % 128 == 0, W % 16 == 0), same slab contract as cdm_conv3x3_wgrad_h3.
  * max|dy| <= *amax_dy from cdm_bn_bwd_amax_bound. */

@@ -43,22 +43,22 @@ class _Recorder:
         raise AttributeError(name)
 
 
-def _dry_run(monkeypatch, nf, B, math):
+def _dry_run(monkeypatch, nf, B, math, H=64):
     protos = LL.parse_header()
     rec = _Recorder(protos)
     monkeypatch.setattr(E, "lib", lambda: rec)
-    eng = E.UNetEngine(nf, 6, 64, "cpu", math)
+    eng = E.UNetEngine(nf, 6, H, "cpu", math)
     from cdm_amd.model import ContextUnet
     torch.manual_seed(0)
-    m = ContextUnet(1, nf, 6, 64, conv_math=math)
+    m = ContextUnet(1, nf, 6, H, conv_math=math)
     P = {k: v.detach().clone() for k, v in list(m.named_parameters()) + list(m.named_buffers())}
     eng.repack(P, True, 0)
     ws = eng.workspace(B, True)
-    x, t, c = torch.rand(B, 64, 64), torch.rand(B), torch.rand(B, 6)
+    x, t, c = torch.rand(B, H, H), torch.rand(B), torch.rand(B, 6)
     sc_w, sc_b = torch.rand(nf), torch.rand(nf)
     eng.forward(ws, P, x, t, c, sc_w, sc_b, B, 0)
     G = {n: torch.empty_like(v) for n, v in m.named_parameters()}
-    deps = torch.rand(B, 64, 64)
+    deps = torch.rand(B, H, H)
     eng.backward(ws, P, deps, G, 0)
     live = []
 
@@ -85,11 +85,12 @@ def _region(live, p):
     return None
 
 
-@pytest.mark.parametrize("nf,B,math", [(128, 2, "h3"), (128, 3, "fp32"), (64, 2, "h3"), (16, 1, "x6"), (128, 256, "h3")])
-def test_launch_arguments_stay_in_bounds(monkeypatch, nf, B, math):
+@pytest.mark.parametrize("nf,B,math,H", [(128, 2, "h3", 64), (128, 3, "fp32", 64), (64, 2, "h3", 64),
+                                         (16, 1, "x6", 64), (128, 256, "h3", 64), (128, 1, "h3", 256)])
+def test_launch_arguments_stay_in_bounds(monkeypatch, nf, B, math, H):
     if nf == 128 and B == 256 and os.environ.get("CDM_BIG_DRYRUN") != "1":
         B = 32                                   # host memory: the full-size workspace is ~20 GB
-    calls, protos, live = _dry_run(monkeypatch, nf, B, math)
+    calls, protos, live = _dry_run(monkeypatch, nf, B, math, H)
     names = _param_names()
     assert len(calls) > 100
     problems = []

@@ -161,14 +161,16 @@ def test_c4_bf16_cfg_sampler_vs_reference_golden(w):
 
 
 # ------------------------------------------------------------------------------------------ C5 (256x256)
-@pytest.mark.parametrize("math", ["fp32", "x6"])
+@pytest.mark.parametrize("math", ["fp32", "x6", "h3"])
 def test_c5_256_forward_vs_oracle(math):
     for train, eps, ref in _forward_pair(16, 256, 1, math):
         assert _rel(eps, ref) < 2e-4, (train, _rel(eps, ref))
 
 
-def test_c5_256_train_grads_vs_fp64():
-    perr, errs, zero_ok, _ = _grad_errors(16, 256, 1, "x6")
+@pytest.mark.parametrize("math", ["x6", "h3"])
+def test_c5_256_train_grads_vs_fp64(math):
+    """h3 at 256x256 runs the wide-row LDS-halo kernel (W 256 / 128) and, at 128x128, the fused BN backward."""
+    perr, errs, zero_ok, _ = _grad_errors(16, 256, 1, math)
     worst = sorted(errs.items(), key=lambda kv: kv[1])[-5:]
     print("pred rel", perr, "worst grads", worst)
     assert perr < 2e-4

@@ -293,7 +293,8 @@ def _conv_h3(L, x, W, b, gy, kc):
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout,kc", [(2, 16, 32, 64, 16), (1, 64, 128, 128, 16), (3, 8, 8, 16, 0),
-                                              (2, 32, 256, 128, 16), (1, 8, 12, 20, 0), (1, 128, 128, 128, 16)])
+                                              (2, 32, 256, 128, 16), (1, 8, 12, 20, 0), (1, 128, 128, 128, 16),
+                                              (1, 256, 32, 128, 16), (2, 128, 64, 256, 16)])
 def test_conv3x3_h3_fp32_class(L, N, H, Cin, Cout, kc):
     """h3 (scaled fp16 hi/lo, 3 products) fwd / dgrad / wgrad at the x6 (fp32) tolerance, and its relative-L2
     error vs an fp64 conv within 4x that of torch's own fp32 CPU conv on the same data.  (torch CPU sums in
@@ -354,7 +355,8 @@ def test_split_f16x2_terms(L):
     assert ((rec - wd).abs() <= bound).all()
 
 
-@pytest.mark.parametrize("N,S,C,Cin", [(2, 64, 128, 128), (2, 32, 256, 128), (1, 32, 128, 256), (2, 32, 256, 256)])
+@pytest.mark.parametrize("N,S,C,Cin", [(2, 64, 128, 128), (2, 32, 256, 128), (1, 32, 128, 256), (2, 32, 256, 256),
+                                       (1, 128, 256, 128)])
 def test_bn_bwd_fused_into_conv_staging_bit_exact(L, N, S, C, Cin):
     """Fused BN backward (dy computed while staging, never written) == norm_apply_bwd mode 0 then the h3
     convs, bit for bit: dgrad (LDS-halo kernel) and wgrad (kernel-row kernel) at the same operand scale; the
