@@ -746,7 +746,8 @@ constexpr int HTHREADS = 512;
 // the second fragment set): 1 fragment prefetch (the next
 // tap's fragments are read during the current tap's MFMAs: 0.94 -> 0.84 ms), 2 every MFMA issued twice, 4 B
 // staged once (stale afterwards), 8 halo stored without the term split, 16 no barriers in the main loop,
-// 32 halo loaded for the first chunk only
+// 32 halo loaded for the first chunk only, 64 / 128 prefetch schedules: 2 reads per MFMA gap / all reads after the
+// tap's first MFMA
 template <int NT, int WT, class EP, bool XCD_REMAP, int ABL = (NT >= 6 ? 0 : 1), class PRE = PreNone>
 __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const float* __restrict__ x, int H, int Cin,
                                                                       int ldx, const __bf16* __restrict__ wx3,
@@ -967,12 +968,25 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
             __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);          // tap 0 fragments
 #pragma unroll
             for (int dx = 0; dx < 2; ++dx) {
+                if constexpr (ABL & 64) {          // two reads per gap: the next tap's fragments land early
 #pragma unroll
-                for (int k = 0; k < RD; ++k) {
+                    for (int k = 0; k < RD / 2; ++k) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x008, MF - RD / 2, 0);
+                } else if constexpr (ABL & 128) {  // all reads after the tap's first MFMA
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, MF - 1, 0);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < RD; ++k) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x008, MF - RD, 0);
                 }
-                __builtin_amdgcn_sched_group_barrier(0x008, MF - RD, 0);
             }
             __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);          // last tap
         }
@@ -1652,6 +1666,8 @@ CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int C
         case 60: CDM_ABL(60); break;
         case 61: CDM_ABL(61); break;
         case 62: CDM_ABL(62); break;
+        case 65: CDM_ABL(65); break;
+        case 129: CDM_ABL(129); break;
         default: return (int)hipErrorInvalidValue;
     }
 #undef CDM_ABL

@@ -5,6 +5,7 @@
   0  shipped kernel            2  every MFMA issued twice (MFMA work x2, staging unchanged)
   1  fragment prefetch         4  B staged only for the first two groups (no per-group B traffic)
   8  halo without the split    12 = 4 + 8 (no B staging, no split)      14 = 12 + 2
+  65 prefetch, 2 fragment reads per MFMA gap      129 prefetch, all reads after the tap's first MFMA
 """
 import json
 import os
@@ -38,7 +39,7 @@ def main(B=256, H=64, C=128, reps=10, relu=True):
     prod = lambda: L.cdm_conv3x3_fwd_h3(x.data_ptr(), B, H, H, C, C, wx.data_ptr(), am.data_ptr(), am.data_ptr() + 4,
                                         b.data_ptr(), y.data_ptr(), C, C, 0, st.data_ptr(), C, 16, None, s)
     fns = {"prod": prod}
-    for abl in (0, 1, 60, 61, 62):
+    for abl in (0, 1, 65, 129, 60, 61, 62):
         fns[abl] = (lambda abl=abl: L.cdm_conv3x3_halo_ablate(
             abl, x.data_ptr(), B, H, C, C, wx.data_ptr(), am.data_ptr(), am.data_ptr() + 4, y.data_ptr(), C, C, s))
     for f in fns.values():

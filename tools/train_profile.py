@@ -15,7 +15,9 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--math", default="h3")
 ap.add_argument("--no-graph", action="store_true")
+ap.add_argument("--c5", action="store_true", help="BASELINE config 5: 256x256, n_feat=256, T=2000, bs=16")
 a = ap.parse_args()
-_, ms, loss = bench.train_rate(bench.NF, bench.H, bench.T, 256, a.math, a.steps, a.warmup, 0,
+nf, H, T, B = (256, 256, 2000, 16) if a.c5 else (bench.NF, bench.H, bench.T, 256)
+_, ms, loss = bench.train_rate(nf, H, T, B, a.math, a.steps, a.warmup, 0,
                                torch.cuda.synchronize, use_graph=not a.no_graph)
-print(f"train {ms:.3f} ms/step = {256 / ms * 1e3:.1f} img/s (math {a.math}, {a.warmup}+{a.steps} steps), loss {loss:.5f}")
+print(f"train {ms:.3f} ms/step = {B / ms * 1e3:.1f} img/s (math {a.math}, {a.warmup}+{a.steps} steps), loss {loss:.5f}")
