@@ -302,11 +302,19 @@ def main():
     args = ap.parse_args()
 
     world, rank, local = _dist_env()
+    # rehearsal of the N>1 path on a one-GPU box: CDM_BENCH_REHEARSE=1 puts every rank on cuda:0 and runs the
+    # collectives over gloo (RCCL refuses two ranks on one device); never set by the driver's runs
+    rehearse = os.environ.get("CDM_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import cdm_amd  # noqa: F401
 
     def barrier():
