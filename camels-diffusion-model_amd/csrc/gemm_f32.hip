@@ -17,6 +17,7 @@
 // ds_read_b32 of 32 consecutive floats per half-wave.  Partial-tile bounds are handled by the
 // loaders (zero fill) and the epilogues (masked stores), so any M and N%4==0, K%4==0 work.
 #include "cdm_common.h"
+#include <cstdlib>
 
 namespace cdm {
 
@@ -730,8 +731,8 @@ struct PreBnBwd {
 
 // ============================== LDS-halo conv3x3 on the split-bf16 matrix cores ==============================
 // conv3x3 (stride 1, pad 1) forward / dgrad for Cin % 16 == 0 (channel-chunk-major K, kc = 16) and image
-// width WT in {32, 64} (128, 256 with the two-term h3 arithmetic).  A block owns 256 consecutive output pixels (= 256/WT whole image rows) x 128
-// output channels, 8 waves as 4 (M) x 2 (N), each wave 64x64.  Per 16-channel chunk the block stages its
+// width WT in {32, 64} (128, 256 with the two-term h3 arithmetic).  A block owns tpb consecutive tiles of 256
+// output pixels (a tile = 256/WT whole image rows) x 128 output channels, one tile after the other, 8 waves as 4 (M) x 2 (N), each wave 64x64.  Per 16-channel chunk the block stages its
 // input rows plus the 1-pixel halo ((256/WT + 2) x (WT + 2) pixels x 16 ch) ONCE into LDS, split into
 // bf16 terms, and the 9 taps of that chunk read their A fragments straight out of the halo tile at
 // shifted addresses: no im2col re-reads (the generic path re-reads every input element 9x through
@@ -752,7 +753,8 @@ template <int NT, int WT, class EP, bool XCD_REMAP, int ABL = (NT >= 6 ? 0 : 1),
 __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const float* __restrict__ x, int H, int Cin,
                                                                       int ldx, const __bf16* __restrict__ wx3,
                                                                       int Cout, const float* amax_x,
-                                                                      const float* amax_w, EP ep, PRE pre) {
+                                                                      const float* amax_w, EP ep, PRE pre,
+                                                                      int mtiles, int tpb) {
     constexpr int NS = XTerms<NT>::NS;
     constexpr int ROWS = HBM_ / WT, HR = ROWS + 2, HC = WT + 2, HPX = HR * HC;
     constexpr int HPLANE = HPX * XBK;                 // bf16 per halo term plane
@@ -765,13 +767,22 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    int bx = blockIdx.x;
+    // the block's tpb 256-pixel tiles, run one after the other: the next tile's first halo and B are fetched
+    // during the current tile's last chunk, so only a block's first tile waits on HBM latency before its MFMAs.
+    // XCD-aware: XCD x owns a contiguous tile range and its cnt blocks step through it together (tile
+    // base + k * cnt + j), so the blocks running at one time hold consecutive tiles whose halo rows meet in L2
+    // (tiles 2j, 2j+1 per block instead put the two rows shared by tiles 2j+1 and 2j+2 in different phases:
+    // measured 1.6x the HBM fetch bytes)
+    int t_first = blockIdx.x * tpb, t_step = 1;
     if constexpr (XCD_REMAP) {
-        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = bx & 7, j = bx >> 3;
-        bx = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+        const int start = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, cnt = xcd < r ? q + 1 : q;
+        t_first = start * tpb + j;
+        t_step = cnt;
     }
-    const int m0 = bx * HBM_, n0 = blockIdx.y * GBN;
-    const int hw = H * WT, img = m0 / hw, h0 = (m0 - img * hw) / WT;
+    if (t_first >= mtiles) return;   // cannot happen for grid.x = ceil(mtiles / tpb); uniform per block
+    const int n0 = blockIdx.y * GBN;
+    const int hw = H * WT;
     const int nchunks = Cin / 16, ngroups = nchunks * 3;
     const float sx = op_scale<NT>(amax_x);
     // BN-backward pre-op: the block's per-channel coefficients, staged once (Cin <= 256)
@@ -785,12 +796,6 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     }
 
     f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     // ---- halo staging: piece q = (halo pixel q>>2, channels 4(q&3)..+3); addresses fixed per block ----
     float4 hreg[HQ];
@@ -798,17 +803,26 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     int hdst[HQ];                   // its LDS offset within a term plane
     float4 yreg[PRE::on ? HQ : 1];  // PreBnBwd: the pre-norm activations of piece j
     const float* hysrc[PRE::on ? HQ : 1];
+    auto setup_tile = [&](int t) {  // halo source addresses of tile t
+        const int m0 = t * HBM_, img = m0 / hw, h0 = (m0 - img * hw) / WT;
+#pragma unroll
+        for (int j = 0; j < HQ; ++j) {
+            const int q = tid + j * HTHREADS;
+            const int hp = q >> 2, c4 = q & 3;
+            const int hr = hp / HC, hc = hp - hr * HC;
+            const int ih = h0 - 1 + hr, iw = hc - 1;
+            const bool in = q < HPX * 4 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)WT;
+            hsrc[j] = in ? x + ((long long)(img * H + ih) * WT + iw) * ldx + c4 * 4 : nullptr;
+            if constexpr (PRE::on)
+                hysrc[j] = in ? pre.y + ((long long)(img * H + ih) * WT + iw) * pre.ldy + c4 * 4 : nullptr;
+        }
+    };
 #pragma unroll
     for (int j = 0; j < HQ; ++j) {
         const int q = tid + j * HTHREADS;
-        const int hp = q >> 2, c4 = q & 3;
-        const int hr = hp / HC, hc = hp - hr * HC;
-        const int ih = h0 - 1 + hr, iw = hc - 1;
-        const bool in = q < HPX * 4 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)WT;
-        hsrc[j] = in ? x + ((long long)(img * H + ih) * WT + iw) * ldx + c4 * 4 : nullptr;
-        if constexpr (PRE::on) hysrc[j] = in ? pre.y + ((long long)(img * H + ih) * WT + iw) * pre.ldy + c4 * 4 : nullptr;
-        hdst[j] = q < HPX * 4 ? xoff(hp, c4 * 4) : -1;
+        hdst[j] = q < HPX * 4 ? xoff(q >> 2, (q & 3) * 4) : -1;
     }
+    setup_tile(t_first);
     auto gload_halo = [&](int cc) {
         if constexpr (ABL & 32) {
             if (cc > 0) return;
@@ -1001,14 +1015,27 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     store_b(Bs, bregA);
     __syncthreads();
     int hb = 0, bb = 0;
+    for (int kt = 0, t = t_first; kt < tpb && t < mtiles; ++kt, t += t_step) {
+    const bool nextt = kt + 1 < tpb && t + t_step < mtiles;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     for (int cc = 0; cc < nchunks; ++cc) {
         const bool morec = cc + 1 < nchunks;
         const int g0 = cc * 3;
         const __bf16* a = Hs + hb * NS * HPLANE;
-        // dy = 0: fetch B of dy = 1 and dy = 2, then the next chunk's halo
+        // dy = 0: fetch B of dy = 1 and dy = 2, then the next chunk's halo (or the next tile's first)
         gload_b(g0 + 1, bregA);
         gload_b(g0 + 2, bregB);
-        if (morec) gload_halo(cc + 1);
+        if (morec) {
+            gload_halo(cc + 1);
+        } else if (nextt) {
+            setup_tile(t + t_step);
+            gload_halo(0);
+        }
         compute(0, a, Bs + bb * BPL * XPLANE);
         store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregA);
         sync();
@@ -1021,6 +1048,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         // dy = 2: fetch B of the next chunk's dy = 0; split + store the next halo (buffer idle since chunk cc-1)
         // ahead of this group's MFMAs, so its VALU work interleaves with them; B after them (just issued)
         if (morec) gload_b(g0 + 3, bregA);
+        else if (nextt) gload_b(0, bregA);
         if (morec) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
         compute(2, a, Bs + bb * BPL * XPLANE);
         if (morec) store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregA);
@@ -1029,7 +1057,14 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         hb ^= 1;
     }
     unscale<NT>(acc, sx, op_scale<NT>(amax_w));
-    ep(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
+    ep(acc, t * HBM_ + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
+    if (nextt) {   // the next tile's chunk 0 (its loads were issued during the last chunk)
+        __syncthreads();                 // the epilogue's scratch aliases the operand LDS
+        store_halo(Hs + hb * NS * HPLANE, 0);
+        store_b(Bs + bb * BPL * XPLANE, bregA);
+        __syncthreads();
+    }
+    }
 }
 
 // ============================== conv3x3 weight gradient, split-bf16, transposed LDS reads ==============================
@@ -1376,29 +1411,43 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
     }
 }
 
+// tiles per block of the LDS-halo conv: as many as keep >= 512 blocks (2 per CU), at most 8.  Kernel level
+// (tools/conv_ablation.py, h3 128->128 @64^2, B=256, one box): 1 tile 0.872 ms, 2: 0.854, 4: 0.848, 8: 0.843,
+// 16: 0.834.  Bench, same box, 2 runs each (tpb 1 -> this policy): C2 train 4296 -> 4355 img/s, sampling 15.94 ->
+// 15.71 ms per step (CFG 31.95 -> 31.50), C4 bf16 train 6416 -> 6478, sample 9.69 -> 9.46 ms, C5 train 70.7 ->
+// 71.2 img/s, sample 69.4 -> 67.6 ms.  The tiles of a block are interleaved across its XCD (see the kernel).
+static int halo_tpb(int mtiles, int ntiles, int nterm, int wt) {
+    (void)nterm; (void)wt;
+    static const int forced = [] { const char* e = getenv("CDM_HALO_TPB"); return e ? atoi(e) : 0; }();
+    if (forced > 0) return forced;   // A/B timing override (tools), never set by the product
+    const int t = (mtiles * ntiles) / 512;
+    return t < 1 ? 1 : (t > 8 ? 8 : t);
+}
+
 template <int WT, class PRE = PreNone>
 static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
                             const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm, hipStream_t s,
-                            PRE pre = PRE{}) {
-    const int M = N * H * WT;
-    dim3 grid(M / HBM_, (Cout + GBN - 1) / GBN, 1);
+                            PRE pre = PRE{}, int tpb = 0) {
+    const int M = N * H * WT, mtiles = M / HBM_;
+    if (tpb < 1) tpb = halo_tpb(mtiles, (Cout + GBN - 1) / GBN, nterm, WT);
+    dim3 grid((mtiles + tpb - 1) / tpb, (Cout + GBN - 1) / GBN, 1);
     if constexpr (WT > 64) {
         // wide rows (C5: 128 / 256 columns): a block is 256 / WT whole rows, halo (256/WT + 2) x (WT + 2);
         // LDS fits the two-term (h3) image only (WT 256: 2 x 2 x 774 px x 32 B + 48 KiB B = 145 KiB)
         if (nterm != NT_H3) return (int)hipErrorInvalidValue;
         hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EpiStoreW<4>, true, 1, PRE>), grid, dim3(HTHREADS), 0, s,
-                           x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre);
+                           x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb);
         return cdm_status();
     } else {
     switch (nterm) {
         case 1: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, (1 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre); break;
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb); break;
         case 3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<3, WT, EpiStoreW<4>, true, (3 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre); break;
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb); break;
         case NT_H3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EpiStoreW<4>, true, (NT_H3 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0,
-                                       s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre); break;
+                                       s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb); break;
         case 6: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<6, WT, EpiStoreW<4>, true, (6 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre); break;
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb); break;
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();
@@ -1645,13 +1694,15 @@ CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int C
                                     const float* amax_x, const float* amax_w, float* y, int ldy, int Cout,
                                     void* stream) {
     if (H != 64 || Cin % 16 || ldx % 4) return (int)hipErrorInvalidValue;
-    const int M = N * H * 64;
+    const int M = N * H * 64, mtiles = M / HBM_;
+    const int tpb = (abl >> 16) > 0 ? (abl >> 16) : 1;   // tiles per block in the high bits (0 -> 1)
+    abl &= 0xffff;
     const EpiStoreW<4> eh{y, ldy, 0, nullptr, Cout, 0, nullptr, 0, M, Cout};
     const __bf16* b = reinterpret_cast<const __bf16*>(wx);
-    dim3 grid(M / HBM_, (Cout + GBN - 1) / GBN, 1);
+    dim3 grid((mtiles + tpb - 1) / tpb, (Cout + GBN - 1) / GBN, 1);
     hipStream_t s = S(stream);
 #define CDM_ABL(A) hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, 64, EpiStoreW<4>, true, A>), grid, dim3(HTHREADS), 0, \
-                                      s, x, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, PreNone{})
+                                      s, x, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, PreNone{}, mtiles, tpb)
     switch (abl) {
         case 0: CDM_ABL(0); break;
         case 1: CDM_ABL(1); break;

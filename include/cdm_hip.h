@@ -54,7 +54,8 @@ int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int ldx, co
                        const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags, float* stats,
                        int stats_ld, int kc, float* amax_y, void* stream);
 /* timing ablations of the h3 LDS-halo conv (64x64 maps, no bias / stats; tools/conv_ablation.py): abl bits
- * 1 fragment prefetch, 2 MFMAs doubled, 4 B staged once, 8 halo without the term split (results meaningless) */
+ * 1 fragment prefetch, 2 MFMAs doubled, 4 B staged once, 8 halo without the term split (results meaningless);
+ * bits 16+: tiles per block (0 -> 1) */
 int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int Cin, int ldx, const void* wx,
                             const float* amax_x, const float* amax_w, float* y, int ldy, int Cout, void* stream);
 int cdm_conv3x3_wgrad_h3(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,

@@ -408,3 +408,24 @@ def test_bn_bwd_fused_into_conv_staging_bit_exact(L, N, S, C, Cin):
                                  amx.data_ptr(), sp, s_got.data_ptr(), _s())
     torch.cuda.synchronize()
     assert torch.equal(s_got, s_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,tpb", [(2, 3), (3, 8), (1, 5)])
+def test_halo_conv_tiles_per_block_bit_exact(L, N, tpb):
+    """Blocks that loop over several 256-pixel tiles (next tile's first halo / B fetched during the last chunk)
+    produce the one-tile-per-block result bit for bit, including a short last block (tiles % tpb != 0)."""
+    H, C = 64, 128
+    g_ = torch.Generator(device="cuda").manual_seed(11)
+    P = N * H * H
+    x = torch.randn(P, C, device="cuda", generator=g_).relu()
+    W = torch.randn(9 * C, C, device="cuda", generator=g_) * 0.05
+    wx, amw = _split_h3(L, W, 9 * C, C)
+    amx = _amax(L, x, P, C)
+    ref = torch.full((P, C), float("nan"), device="cuda"); got = torch.full_like(ref, float("nan"))
+    for out, t in ((ref, 1), (got, tpb)):
+        assert L.cdm_conv3x3_halo_ablate(1 | (t << 16), x.data_ptr(), N, H, C, C, wx.data_ptr(), amx.data_ptr(),
+                                         amw.data_ptr(), out.data_ptr(), C, C, _s()) == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(ref).all()
+    assert torch.equal(got, ref)

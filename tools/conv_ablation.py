@@ -6,6 +6,7 @@
   1  fragment prefetch         4  B staged only for the first two groups (no per-group B traffic)
   8  halo without the split    12 = 4 + 8 (no B staging, no split)      14 = 12 + 2
   65 prefetch, 2 fragment reads per MFMA gap      129 prefetch, all reads after the tap's first MFMA
+  bits 16+: tiles per block (1 | 8 << 16 = the shipped kernel at this shape: 8 256-pixel tiles per block)
 """
 import json
 import os
@@ -39,7 +40,7 @@ def main(B=256, H=64, C=128, reps=10, relu=True):
     prod = lambda: L.cdm_conv3x3_fwd_h3(x.data_ptr(), B, H, H, C, C, wx.data_ptr(), am.data_ptr(), am.data_ptr() + 4,
                                         b.data_ptr(), y.data_ptr(), C, C, 0, st.data_ptr(), C, 16, None, s)
     fns = {"prod": prod}
-    for abl in (0, 1, 65, 129, 60, 61, 62):
+    for abl in (1, 1 | 2 << 16, 1 | 4 << 16, 1 | 8 << 16, 1 | 16 << 16, 61):
         fns[abl] = (lambda abl=abl: L.cdm_conv3x3_halo_ablate(
             abl, x.data_ptr(), B, H, C, C, wx.data_ptr(), am.data_ptr(), am.data_ptr() + 4, y.data_ptr(), C, C, s))
     for f in fns.values():
@@ -56,7 +57,8 @@ def main(B=256, H=64, C=128, reps=10, relu=True):
             e1.synchronize()
             times[k].append(e0.elapsed_time(e1) / reps)
     for k, v in times.items():
-        out[k] = round(sorted(v)[len(v) // 2], 4)
+        key = k if k == "prod" or k < 65536 else f"{k & 0xffff}/tpb{k >> 16}"
+        out[key] = round(sorted(v)[len(v) // 2], 4)
     print(json.dumps(out))
 
 
