@@ -246,19 +246,53 @@ using EpiStore = EpiStoreW<2>;
 struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n, 2h+i, 2w+j, co] = acc + b[co]
     float* y; long long ldy; const float* bias; int H, W, Co, M, N;
     float* amax = nullptr;       // optional running max|y| (block_amax_commit)
+    // Integer divisions only per lane and row block / column (6 per lane, not 2 per element: the per-element form
+    // spent more issue cycles on v_rcp_iflag / v_mul_lo sequences than the K = Cin main loop on MFMAs).  The 16 rows
+    // of an accumulator are mw + 32 i + 4 (lane >> 5) + {0..3, 8..11, 16..19, 24..27}: (b, h, w) advance by carry.
     __device__ __forceinline__ void operator()(f32x16 (&acc)[2][2], int mw, int nw, int lane, int, int,
                                                float*, int) const {
         float am = 0.f;
-        CDM_FOR_ACC({
-            if (m < M && n < N) {
-                const int hw = H * W; const int b = m / hw; const int rem = m - b * hw;
-                const int h = rem / W, w = rem - h * W;
-                const int ij = n / Co, co = n - ij * Co;
-                float v = acc[i][j][r] + (bias ? bias[co] : 0.f);
-                y[((long long)(b * 2 * H + 2 * h + (ij >> 1)) * (2 * W) + 2 * w + (ij & 1)) * ldy + co] = v;
-                am = fmaxf(am, fabsf(v));
+        const int hw = H * W;
+        long long coff[2];   // output offset of column n inside its 2x2 block: (ij >> 1) rows, (ij & 1) pixels, co
+        float bj[2];
+        bool nok[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = nw + 32 * j + (lane & 31);
+            nok[j] = n < N;
+            const int ij = nok[j] ? n / Co : 0, co = nok[j] ? n - ij * Co : 0;
+            coff[j] = ((long long)(ij >> 1) * (2 * W) + (ij & 1)) * ldy + co;
+            bj[j] = bias ? bias[co] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int mb = mw + 32 * i + 4 * (lane >> 5);
+            int b = mb / hw;
+            const int rem = mb - b * hw;
+            int h = rem / W, w = rem - h * W;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int d = (r & 3) + 8 * (r >> 2);
+                if (r > 0) {
+                    w += d - ((r - 1) & 3) - 8 * ((r - 1) >> 2);
+                    while (w >= W) {
+                        w -= W;
+                        if (++h == H) { h = 0; ++b; }
+                    }
+                }
+                if (mb + d < M) {
+                    const long long pb = ((long long)(b * 2 * H + 2 * h) * (2 * W) + 2 * w) * ldy;
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        if (nok[j]) {
+                            const float v = acc[i][j][r] + bj[j];
+                            y[pb + coff[j]] = v;
+                            am = fmaxf(am, fabsf(v));
+                        }
+                    }
+                }
             }
-        })
+        }
         if (amax) block_amax_commit(am, amax);
     }
 };
