@@ -74,7 +74,7 @@ struct LdConvT2x2GatherA {  // dgrad of convT 2x2: m = (n,h,w) on the INPUT grid
     }
     __device__ __forceinline__ float4 load(const Row& r, int k) const {
         if (!r.ok || k >= K) return f4zero();
-        const int ij = k / Co, co = k - ij * Co;
+        const int ij = (k >= Co) + (k >= 2 * Co) + (k >= 3 * Co), co = k - ij * Co;   // k < K = 4 Co: no division
         const int oh = 2 * r.h + (ij >> 1), ow = 2 * r.w + (ij & 1);
         return ld4(dy + ((long long)(r.n * 2 * H + oh) * (2 * W) + ow) * lddy + co);
     }
