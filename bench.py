@@ -117,17 +117,14 @@ def pmc_traffic(math: str):
     return int(d["traffic_bytes"])
 
 
-def cpu_baseline(threads: int):
-    """Reference algorithm (CPU oracle, torch CPU fp32) on a bounded sample of the same workload."""
-    from oracle import ref_cpu as R
-    torch.set_num_threads(threads)
-    bs = 16
-    torch.manual_seed(0)
-    import cdm_amd  # noqa: F401  (only for the reference-identical seeded parameter init)
+def _cpu_train_rate(R, nf: int, T: int, bs: int, steps: int, warmup: int):
+    """Train steps (perturb + fwd + mse + bwd + Adam) of the CPU oracle at batch bs -> seconds per step."""
     from cdm_amd.model import ContextUnet
-    m = ContextUnet(1, NF, NCF, H)
+    torch.manual_seed(0)
+    m = ContextUnet(1, nf, NCF, H)                  # only for the reference-identical seeded parameter init
     sd = R.clone_sd(m.state_dict())
-    tr = R.OracleTrainer(sd, n_feat=NF, n_cfeat=NCF, height=H, lr=1e-5)
+    del m
+    tr = R.OracleTrainer(sd, n_feat=nf, n_cfeat=NCF, height=H, lr=1e-5)
     _, _, ab = R.make_schedule(T)
     g = torch.Generator().manual_seed(1234)
     x = torch.rand(bs, 1, H, H, generator=g); c = torch.rand(bs, NCF, generator=g)
@@ -135,29 +132,66 @@ def cpu_baseline(threads: int):
     def one():
         noise = torch.randn(bs, 1, H, H, generator=g)
         t = torch.randint(1, T + 1, (bs,), generator=g)
-        tr.step(x, c, noise, t, T, ab, lambda: R.draw_shortcut(1, NF))
+        tr.step(x, c, noise, t, T, ab, lambda: R.draw_shortcut(1, nf))
 
-    one()                                   # warm-up
-    steps = 2
+    for _ in range(warmup):
+        one()
     t0 = time.perf_counter()
     for _ in range(steps):
         one()
-    dt = (time.perf_counter() - t0) / steps
-    # one sampling step (eval forward) at the same batch, extrapolated to T steps
-    fn = R.make_model_fn(sd, n_feat=NF, n_cfeat=NCF, height=H)
-    xs = torch.randn(bs, 1, H, H)
-    tt = torch.tensor([0.5])
-    fn(xs, tt, c)
+    return (time.perf_counter() - t0) / steps, tr.sd
+
+
+def _cpu_sample_rate(R, sd, nf: int, T: int, n: int, w: float, steps: int):
+    """`steps` reverse-diffusion steps of the reference sampler (code/train_diffusion_condition.py:312-329: z draw,
+    cond (+ uncond) eval forward with its fresh shortcut, CFG combine, denoise_add_noise) -> seconds per step."""
+    b, a, ab = R.make_schedule(T)
+    fn = R.make_model_fn(sd, n_feat=nf, n_cfeat=NCF, height=H)
+    g = torch.Generator().manual_seed(99)
+    x = torch.randn(n, 1, H, H, generator=g)
+    params = torch.rand(n, NCF, generator=g)
+    uncond = torch.zeros_like(params)
     t0 = time.perf_counter()
-    fn(xs, tt, c)
-    ds = time.perf_counter() - t0
+    for i in range(T, T - steps, -1):
+        t = torch.tensor([i / T])
+        z = torch.randn(x.shape, generator=g)
+        if w > 0:
+            ec = fn(x, t, params); eu = fn(x, t, uncond)
+            eps = eu + w * (ec - eu)
+        else:
+            eps = fn(x, t, params)
+        x = R.denoise_add_noise(x, i, eps, z, b, a, ab)
+    return (time.perf_counter() - t0) / steps
+
+
+def cpu_baseline(threads: int):
+    """The reference algorithm (CPU oracle = torch CPU fp32 restatement, pinned bit-exact to the reference's own
+    outputs) on the host cores, per BASELINE.md §3: C2 train step at bs=256 timed directly (1 warm-up + 2 steps),
+    3 sampling steps at n=256 for w=0 and w=1 extrapolated to T=1500, and config C1 (n_feat=64, bs=8, T=1000)."""
+    from oracle import ref_cpu as R
+    torch.set_num_threads(threads)
+    bs = 256
+    dt, sd = _cpu_train_rate(R, NF, T, bs, steps=2, warmup=1)
+    S = 3
+    s0 = _cpu_sample_rate(R, sd, NF, T, bs, 0.0, S)
+    s1 = _cpu_sample_rate(R, sd, NF, T, bs, 1.0, S)
+    del sd
+    # C1 (BASELINE.json configs[0]): n_feat=64, bs=8, T=1000
+    T1 = 1000
+    dt1, sd1 = _cpu_train_rate(R, 64, T1, 8, steps=5, warmup=1)
+    s01 = _cpu_sample_rate(R, sd1, 64, T1, 8, 0.0, 10)
     return {
         "value": bs / dt, "unit": "images/s", "cores": threads, "kind": "port",
-        "sample": f"{steps} train steps (fwd+bwd+Adam) at bs={bs}, n_feat=128, 64x64, after 1 warm-up; "
-                  f"CPU oracle = torch CPU fp32 restatement of the reference path",
-        "ms_per_step": dt * 1e3,
-        "sample_img_per_s_extrapolated": bs / (ds * T),
-        "sample_note": f"1 eval forward at n={bs} timed ({ds*1e3:.0f} ms) and extrapolated x{T} steps",
+        "sample": f"C2 shape: 2 train steps (perturb + fwd + mse + bwd + Adam) at bs={bs}, n_feat=128, 64x64, timed "
+                  f"directly after 1 warm-up step; CPU oracle = torch CPU fp32 restatement of the reference path",
+        "ms_per_step": round(dt * 1e3, 1),
+        "sample_img_per_s_extrapolated": {"w=0": bs / (s0 * T), "w=1": bs / (s1 * T)},
+        "sample_note": f"{S} reverse-diffusion steps at n={bs} timed per guide weight ({s0 * 1e3:.0f} / "
+                       f"{s1 * 1e3:.0f} ms per step for w=0 / w=1) and extrapolated x{T} steps",
+        "c1": {"workload": "C1: n_feat=64, 6 params, 64x64, T=1000, bs=8 (BASELINE configs[0], the reference's CPU "
+                           "case)", "train_img_per_s": round(8 / dt1, 3), "train_ms_per_step": round(dt1 * 1e3, 1),
+               "train_steps": 5, "sample_ms_per_step": round(s01 * 1e3, 1),
+               "sample_img_per_s_extrapolated": 8 / (s01 * T1), "sample_steps_run": 10},
     }
 
 

@@ -527,13 +527,17 @@ __global__ __launch_bounds__(256) void mse_kernel(const float* pred, const float
         partial[blockIdx.x * 2 + 1] = r1[0] + r1[1] + r1[2] + r1[3];
     }
 }
-// loss = sum0 / numel (written to loss_out), dbias = sum1 (written to dbias_out)
-__global__ void mse_finalize_kernel(const float* partial, int nb, double inv_numel, float* loss_out, float* dbias_out) {
+// loss = sum0 / numel (written to loss_out), dbias = sum1 (written to dbias_out); nonfinite (optional) counts
+// the steps whose loss is NaN / inf (the trainer's failure guard, read once per epoch: no per-step host sync)
+__global__ void mse_finalize_kernel(const float* partial, int nb, double inv_numel, float* loss_out, float* dbias_out,
+                                    int* nonfinite) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     double a = 0.0, b = 0.0;
     for (int i = 0; i < nb; ++i) { a += partial[2 * i]; b += partial[2 * i + 1]; }
-    if (loss_out) *loss_out = (float)(a * inv_numel);
+    const float loss = (float)(a * inv_numel);
+    if (loss_out) *loss_out = loss;
     if (dbias_out) *dbias_out = (float)b;
+    if (nonfinite && !isfinite(loss)) *nonfinite += 1;
 }
 
 // Sampler step prologue (device-side step counter, so one captured step replays for every i):
@@ -552,17 +556,20 @@ __global__ void sample_prologue_kernel(int* ctr, int T, int* cur_i, float* t_cur
 // Writes x into both halves of the model-input buffer (x2 may alias x), and a snapshot when slot[i] >= 0.
 __global__ void denoise_kernel(const float* xin, float* x, float* x2, long long numel, const float* eps, int cfg,
                                float w, const int* cur_i, const float* coef, const float* sa, const float* sb,
-                               const float* z_table, long long zstride, unsigned long long seed, const int* snap_slot,
-                               float* snaps, int T) {
+                               const float* z_table, long long zstride, unsigned long long seed,
+                               const long long* seed_dev, const int* snap_slot, float* snaps, int T) {
 #pragma clang fp contract(off)  // keep the reference's separate fp32 roundings (bit-exact)
     const int i = *cur_i;
     const float cf = coef[i], a = sa[i], b = sb[i];
     const int slot = snap_slot ? snap_slot[i] : -1;
+    // per-run key: seed ^ *seed_dev (drawn from torch's CUDA generator before every run, so consecutive sampling
+    // calls get fresh z, as the reference's randn_like on the device does)
+    const unsigned long long sd = seed_dev ? seed ^ (unsigned long long)seed_dev[0] : seed;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < numel; e += (long long)gridDim.x * blockDim.x) {
         float ep = eps[e];
         if (cfg) { const float eu = eps[numel + e]; ep = eu + w * (ep - eu); }
         float z = 0.f;
-        if (i > 1) z = z_table ? z_table[(long long)(T - i) * zstride + e] : philox_normal(seed, (uint32_t)i, e);
+        if (i > 1) z = z_table ? z_table[(long long)(T - i) * zstride + e] : philox_normal(sd, (uint32_t)i, e);
         const float mean = (xin[e] - ep * cf) / a;   // same op order / roundings as the reference
         const float v = mean + b * z;
         x[e] = v;
@@ -572,28 +579,42 @@ __global__ void denoise_kernel(const float* xin, float* x, float* x2, long long 
 }
 
 // ------------------------------------------------------------------------------------------------
-// Adam (torch single-tensor arithmetic), lr/step in device memory so a captured step replays.
-// state: [0] lr, [1] step (float count), [2] -step_size, [3] sqrt(bias_correction2)
+// Adam = torch.optim.Adam's single-tensor step (torch/optim/adam.py _single_tensor_adam, the path the
+// reference's CPU run takes; code/train_diffusion_condition.py:200,229), with lr / step in device memory so
+// a captured step replays.
+// state (double[4]): [0] lr (a Python float, as torch keeps it), [1] step count, [2] -step_size rounded to
+//                    fp32, [3] sqrt(bias_correction2) rounded to fp32
+// bc (double[nbc][2]): 1 - beta1**step and (1 - beta2**step)**0.5 for step = 1..nbc, evaluated on the host
+//                    with torch's own Python-double expressions (the last row is exactly {1, 1}; steps past
+//                    nbc reuse it, which is exact since both powers have underflowed below 2^-54 there)
+// Elementwise roundings follow torch's CPU kernels (probed against torch 2.10 AVX-512):
+//   exp_avg.lerp_(g, 1-b1)           lerp_vec: fmadd(w, g - m, m)                 -> one fma
+//   exp_avg_sq.mul_(b2)              v * float(b2)
+//              .addcmul_(g, g, 1-b2)   self + (c * g) * g, contracted to fma(c*g, g, self)
+//   denom = sqrt(v) / bc2s + eps     div by the fp32-cast scalar, add (alpha = 1)
+//   param.addcdiv_(m, denom, -ss)    self + (value * m) / denom
+// The one deliberate difference: sqrtf here is correctly rounded; torch's vectorised CPU sqrt is not always
+// (<= 1 ulp), so p differs from torch CPU by <= 1 ulp of the update on those elements (test_gpu_trainer.py).
 // ------------------------------------------------------------------------------------------------
-__global__ void adam_prep_kernel(float* state, double beta1, double beta2) {
-    const double step = (double)state[1] + 1.0;
-    state[1] = (float)step;
-    const double bc1 = 1.0 - pow(beta1, step), bc2 = 1.0 - pow(beta2, step);
-    state[2] = (float)(-(double)state[0] / bc1);
-    state[3] = (float)sqrt(bc2);
+__global__ void adam_prep_kernel(double* state, const double* bc, int nbc) {
+    const double step = state[1] + 1.0;
+    state[1] = step;
+    const int k = (int)(step < (double)nbc ? step : (double)nbc) - 1;
+    state[2] = (double)(float)(-(state[0] / bc[2 * k]));     // value=-step_size, Scalar -> float
+    state[3] = (double)(float)bc[2 * k + 1];                  // bias_correction2_sqrt, wrapped scalar -> float
 }
-__global__ void adam_kernel(float* p, const float* g, float* m, float* v, long long n, const float* state, float beta1c,
+__global__ void adam_kernel(float* p, const float* g, float* m, float* v, long long n, const double* state, float beta1c,
                             float beta2, float beta2c, float eps, float gscale) {
-#pragma clang fp contract(off)  // keep the reference's separate fp32 roundings (bit-exact)
-    const float nss = state[2], bc2s = state[3];
+#pragma clang fp contract(off)  // only the explicit fmaf below fuse, as in torch's CPU kernels
+    const float nss = (float)state[2], bc2s = (float)state[3];
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
         const float gi = g[i] * gscale;             // 1/world for the summed data-parallel gradient
         float mi = m[i];
-        mi = mi + beta1c * (gi - mi);                    // exp_avg.lerp_(grad, 1 - beta1)
+        mi = fmaf(beta1c, gi - mi, mi);                   // exp_avg.lerp_(grad, 1 - beta1)
         float vi = v[i] * beta2;                          // exp_avg_sq.mul_(beta2)
-        vi = vi + beta2c * gi * gi;                       //   .addcmul_(grad, grad, 1 - beta2)
+        vi = fmaf(beta2c * gi, gi, vi);                   //   .addcmul_(grad, grad, 1 - beta2)
         const float denom = sqrtf(vi) / bc2s + eps;       // (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
-        p[i] = p[i] + nss * (mi / denom);                 // param.addcdiv_(exp_avg, denom, -step_size)
+        p[i] = p[i] + (nss * mi) / denom;                 // param.addcdiv_(exp_avg, denom, -step_size)
         m[i] = mi; v[i] = vi;
     }
 }
@@ -782,13 +803,14 @@ CDM_API int cdm_mse_accum(const float* pred, const float* noise, long long nstri
                        div, acc);
     return cdm_status();
 }
-CDM_API int cdm_mse(const float* pred, const float* noise, long long n, float* dpred, float* partial, int nb,
-                    float* loss_out, float* dbias_out, void* stream) {
-    hipLaunchKernelGGL(mse_kernel, dim3(nb), dim3(256), 0, S(stream), pred, noise, n, (float)(2.0 / (double)n), dpred,
+CDM_API int cdm_mse(const float* pred, const float* noise, long long n, double grad_numel, float* dpred, float* partial,
+                    int nb, float* loss_out, float* dbias_out, int* nonfinite, void* stream) {
+    if (!(grad_numel > 0.0)) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(mse_kernel, dim3(nb), dim3(256), 0, S(stream), pred, noise, n, (float)(2.0 / grad_numel), dpred,
                        partial);
     int e = cdm_status(); if (e) return e;
     hipLaunchKernelGGL(mse_finalize_kernel, dim3(1), dim3(64), 0, S(stream), partial, nb, 1.0 / (double)n, loss_out,
-                       dbias_out);
+                       dbias_out, nonfinite);
     return cdm_status();
 }
 CDM_API int cdm_sample_prologue(int* ctr, int T, int* cur_i, float* t_cur, const float* sc_table, int sc_row, float* sc_cur,
@@ -799,15 +821,16 @@ CDM_API int cdm_sample_prologue(int* ctr, int T, int* cur_i, float* t_cur, const
 }
 CDM_API int cdm_denoise(const float* xin, float* x, float* x2, long long numel, const float* eps, int cfg, float w,
                         const int* cur_i, const float* coef, const float* sa, const float* sb, const float* z_table,
-                        long long zstride, unsigned long long seed, const int* snap_slot, float* snaps, int T,
-                        void* stream) {
+                        long long zstride, unsigned long long seed, const long long* seed_dev, const int* snap_slot,
+                        float* snaps, int T, void* stream) {
     hipLaunchKernelGGL(denoise_kernel, dim3(nblocks(numel)), dim3(256), 0, S(stream), xin, x, x2, numel, eps, cfg, w, cur_i,
-                       coef, sa, sb, z_table, zstride, seed, snap_slot, snaps, T);
+                       coef, sa, sb, z_table, zstride, seed, seed_dev, snap_slot, snaps, T);
     return cdm_status();
 }
-CDM_API int cdm_adam(float* p, const float* g, float* m, float* v, long long n, float* state, double beta1, double beta2,
-                     double eps, float grad_scale, void* stream) {
-    hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, S(stream), state, beta1, beta2);
+CDM_API int cdm_adam(float* p, const float* g, float* m, float* v, long long n, double* state, const double* bc,
+                     int nbc, double beta1, double beta2, double eps, float grad_scale, void* stream) {
+    if (nbc < 1) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, S(stream), state, bc, nbc);
     int e = cdm_status(); if (e) return e;
     hipLaunchKernelGGL(adam_kernel, dim3(nblocks(n, 256, 16384)), dim3(256), 0, S(stream), p, g, m, v, n, state,
                        (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, grad_scale);

@@ -46,12 +46,19 @@ class Schedule:
     """b_t, a_t, ab_t (T+1) computed with the reference's fp32 expressions on the host, plus the
     per-step coefficient tables the kernels read (same fp32 operations as the reference)."""
 
-    def __init__(self, timesteps: int, device="cuda", beta1: float = BETA1, beta2: float = BETA2):
+    def __init__(self, timesteps: int, device="cuda", beta1: float = BETA1, beta2: float = BETA2, tensors=None):
+        """``tensors=(b_t, a_t, ab_t)`` uses a caller's schedule (the functional sampler of
+        code/sample_power_spectra.py:71-110 takes them as arguments) instead of building the default one."""
         self.T = int(timesteps)
-        b_t = (beta2 - beta1) * torch.linspace(0, 1, self.T + 1) + beta1
-        a_t = 1 - b_t
-        ab_t = torch.cumsum(a_t.log(), dim=0).exp()
-        ab_t[0] = 1
+        if tensors is not None:
+            b_t, a_t, ab_t = (torch.as_tensor(v).detach().to("cpu", torch.float32).reshape(-1) for v in tensors)
+            if not (b_t.numel() == a_t.numel() == ab_t.numel() == self.T + 1):
+                raise ValueError(f"schedule tensors must have timesteps + 1 = {self.T + 1} entries")
+        else:
+            b_t = (beta2 - beta1) * torch.linspace(0, 1, self.T + 1) + beta1
+            a_t = 1 - b_t
+            ab_t = torch.cumsum(a_t.log(), dim=0).exp()
+            ab_t[0] = 1
         dev = torch.device(device)
         self.b_t, self.a_t, self.ab_t = b_t.to(dev), a_t.to(dev), ab_t.to(dev)
         self.sab = ab_t.sqrt().to(dev)                       # perturb: sqrt(ab[t])
@@ -95,7 +102,7 @@ def denoise_add_noise(x, t: int, pred_noise, z, sched: Schedule):
     T = max(int(t), sched.T)
     # z_table with stride 0: z[e] for every step; force i > 1 semantics by the table itself
     lib().cdm_denoise(_p(x), _p(out), None, x.numel(), _p(pred_noise), 0, 0.0, _p(cur), _p(sched.coef),
-                      _p(sched.sa), _p(sched.sb), _p(z), 0, 0, None, None, T, _s())
+                      _p(sched.sa), _p(sched.sb), _p(z), 0, 0, None, None, None, T, _s())
     if int(t) <= 1 and z.abs().max().item() != 0:  # kernel treats i == 1 as z = 0 (reference passes 0 there)
         out = out + sched.b_t.sqrt()[int(t)] * z
     return out
@@ -154,6 +161,7 @@ class GraphSampler:
         self.slot = torch.from_numpy(slots).to(dev) if snapshots else None
         self.snaps = E(max(self.nslots, 1), n * H * H)
         self.z_table = E(max(self.T - 1, 1), n * H * H) if z_source == "host" else None
+        self.zseed = torch.zeros(1, dtype=torch.int64, device=dev)    # per-run Philox key (device z mode)
         self.K = max(1, int(steps_per_graph))
         self.use_graph = use_graph
         self.graph = None
@@ -192,8 +200,8 @@ class GraphSampler:
         numel = n * self.H * self.H
         lb.cdm_denoise(_p(self.xbuf), _p(self.xbuf), _p(self.xbuf) if self.cfg else None, numel, _p(eps),
                        1 if self.cfg else 0, self.guide_w, _p(self.cur_i), _p(self.sched.coef), _p(self.sched.sa),
-                       _p(self.sched.sb), _p(self.z_table), numel, self.seed, _p(self.slot), _p(self.snaps),
-                       self.T, s)
+                       _p(self.sched.sb), _p(self.z_table), numel, self.seed, _p(self.zseed), _p(self.slot),
+                       _p(self.snaps), self.T, s)
 
     def _capture(self):
         s = torch.cuda.Stream()
@@ -226,6 +234,10 @@ class GraphSampler:
         self.prepare()
         total = self.T if steps is None else min(int(steps), self.T)
         self.xbuf[:n] = x_T.to(self.dev, torch.float32).reshape(n, H, H)
+        if self.z_source == "device":
+            # fresh z for every run, drawn from torch's CUDA generator (the reference's randn_like(x) on the device
+            # consumes it too): reproducible under torch.cuda.manual_seed, different across consecutive calls
+            self.zseed.random_(generator=None)
         if self.cfg:
             self.xbuf[n:] = self.xbuf[:n]
         self.ctr.fill_(self.T)
@@ -248,9 +260,10 @@ class GraphSampler:
 class DDPM:
     """Script-globals bundle of the reference (nn_model, timesteps, b_t/a_t/ab_t, n_cfeat, device)."""
 
-    def __init__(self, model, timesteps: int, device="cuda", z_source: str = "device", seed: int = 1234):
+    def __init__(self, model, timesteps: int, device="cuda", z_source: str = "device", seed: int = 1234,
+                 sched_tensors=None):
         self.model, self.T = model, int(timesteps)
-        self.sched = Schedule(self.T, device)
+        self.sched = Schedule(self.T, device, tensors=sched_tensors)
         self.b_t, self.a_t, self.ab_t = self.sched.tensors()
         self.device = torch.device(device)
         self.n_cfeat = model.n_cfeat
@@ -298,8 +311,13 @@ class DDPM:
 @torch.no_grad()
 def sample_ddpm(model, n_sample=1, size=64, device=None, params=None, guide_w=0.0, timesteps=1000, b_t=None,
                 a_t=None, ab_t=None, z_source="device"):
-    """Functional sampler of code/sample_power_spectra.py:71-110 (returns the final x only)."""
-    d = DDPM(model, timesteps, device or model.out[3].weight.device, z_source=z_source)
+    """Functional sampler of code/sample_power_spectra.py:71-110 (returns the final x only).  b_t / a_t / ab_t are
+    the caller's schedule, as in the reference (all three or none: None builds the default schedule)."""
+    given = [v is not None for v in (b_t, a_t, ab_t)]
+    if any(given) and not all(given):
+        raise ValueError("pass all of b_t, a_t, ab_t or none of them")
+    d = DDPM(model, timesteps, device or model.out[3].weight.device, z_source=z_source,
+             sched_tensors=(b_t, a_t, ab_t) if all(given) else None)
     if params is None:
         x_T = torch.randn(n_sample, 1, size, size)
         params = torch.rand(n_sample, 6 if model.n_cfeat == 6 else model.n_cfeat)

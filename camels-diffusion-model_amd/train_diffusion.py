@@ -13,6 +13,9 @@ Positional arguments keep the reference semantics:
           every 5 epochs, checkpoints model_epoch_{ep+1}.pth every 25 epochs and at the end; then CFG sampling
           and conditioned reconstruction of held-out maps.
 Per epoch the learning rate is lr*(1 - ep/E) (:213); batch size 32, n_feat 128, 64x64 (:82-85).
+Data parallel (torchrun, N ranks): --batch-size is per rank, each step is one global batch of N x batch-size
+samples of the epoch's permutation split across the ranks (trainer.shard_epoch), and an epoch whose loss turned
+NaN / inf stops the run (device-side counter, one read per epoch).
 
 Data (code/train_diffusion_condition.py:104-160): Maps_HI_IllustrisTNG_LH_z=0.00.npy [N,256,256] -> shift
 to positive, /max, log10, min-max to [0,1], bilinear to 64x64; params.npy [N/15, 6] repeated x15, per-column
@@ -66,6 +69,7 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import cdm_amd
     from cdm_amd import DDPM, ContextUnet, Trainer
+    from cdm_amd.trainer import shard_epoch
 
     conditional = a.num_params is not None
     n_cfeat = a.num_params if conditional else 5
@@ -118,13 +122,18 @@ def main(argv=None):
         trainer.set_lr(lr)
         model.train()
         order = train_idx[torch.randperm(len(train_idx), generator=torch.Generator().manual_seed(a.seed * 7919 + ep))]
-        order = order[rank::world]
         ep_loss, nb = torch.zeros(1, device=dev), 0
-        for i in range(0, len(order), a.batch_size):
-            idx = order[i:i + a.batch_size].to(dev)
-            loss = trainer.step(maps_d[idx], params_d[idx] if conditional else None)
+        # every rank runs the same number of steps; ragged global batches are weighted by sample count
+        for idx, count in shard_epoch(order, a.batch_size, world, rank):
+            idx = idx.to(dev)
+            loss = trainer.step(maps_d[idx], params_d[idx] if conditional else None,
+                                global_count=count if world > 1 and count != a.batch_size * world else None)
             ep_loss += loss
             nb += 1
+        bad = trainer.check_finite()                 # SURVEY §5 failure guard: one host read per epoch
+        if bad:
+            raise FloatingPointError(f"epoch {ep + 1}: {bad} training step(s) produced a NaN / inf loss "
+                                     f"(lr {lr:.3e}); stopping before the checkpoint is overwritten")
         torch.cuda.synchronize()
         ep_time = time.time() - t_ep
         loss_log.append(float(ep_loss.item()) / max(nb, 1))

@@ -134,8 +134,12 @@ class Trainer:
             dist.broadcast(self.flat, 0, group=group)
             dist.broadcast(self.bnflat, 0, group=group)
             self.bucketer = GradBucketer(self.gflat, self.ranges, group)
-        # ---- optimizer state on device: [lr, step, -step_size, sqrt(bc2)] ----
-        self.opt_state = torch.tensor([float(lrate), 0.0, 0.0, 1.0], device=dev)
+        # ---- optimizer state on device (fp64, as torch keeps lr / step as Python floats):
+        #      [lr, step, -step_size, sqrt(bc2)] + the host-evaluated bias-correction table ----
+        self.betas, self.eps = (0.9, 0.999), 1e-8
+        self.opt_state = torch.tensor([float(lrate), 0.0, 0.0, 1.0], dtype=torch.float64, device=dev)
+        self.adam_bc = adam_bias_table(*self.betas).to(dev)
+        self.nonfinite = torch.zeros(1, dtype=torch.int32, device=dev)   # steps with a NaN / inf loss
         # ---- step buffers (per batch size: the epoch's ragged last batch gets its own) ----
         self.sched = Schedule(self.T, dev)
         self.sc = torch.empty(2 * self.nf, device=dev)
@@ -149,6 +153,8 @@ class Trainer:
         self.graph = None
         self.steps = 0
         self._inject = None
+        self.stage_hook = None        # optional extra on_stage(name) callback (tests / tracing)
+        self.grad_numel = None        # per-step override of the loss-mean count (data-parallel ragged batches)
 
     # -------------------------------------------------------------------------------------------
     def _use(self, B: int):
@@ -171,7 +177,16 @@ class Trainer:
         return P
 
     def set_lr(self, lr: float):
+        """optim.param_groups[0]['lr'] = lr (code/train_diffusion_condition.py:213); exact Python-float lr."""
         self.opt_state[0:1].fill_(float(lr))
+
+    def check_finite(self, reset: bool = True) -> int:
+        """Number of steps since the last check whose loss was NaN / inf (SURVEY §5 failure guard).  One host sync:
+        call it once per epoch, not per step."""
+        n = int(self.nonfinite.item())
+        if reset and n:
+            self.nonfinite.zero_()
+        return n
 
     def _body(self, s: int):
         lb = lib()
@@ -215,13 +230,19 @@ class Trainer:
             self._body(torch.cuda.current_stream().cuda_stream)
         self.graph = g
 
-    def step(self, x0: Optional[torch.Tensor] = None, c: Optional[torch.Tensor] = None, inject=None) -> torch.Tensor:
+    def step(self, x0: Optional[torch.Tensor] = None, c: Optional[torch.Tensor] = None, inject=None,
+             global_count: Optional[int] = None) -> torch.Tensor:
         """One training step on batch (x0 [B,1,H,H] in [0,1], c [B, n_cfeat] or None = unconditional).
 
         ``inject=(noise [B,1,H,H], t [B] int, shortcut [2*n_feat] = weight|bias)`` replaces the on-device
-        Philox draws for this step (parity testing; runs eagerly)."""
+        Philox draws for this step (parity testing; runs eagerly).
+        ``global_count`` (data parallel): the number of samples all ranks process in this step when the ranks'
+        batches differ in size; the gradient is then the mean over those samples (each rank weighted by its
+        sample count, F.mse_loss over the union) instead of the mean of per-rank means."""
         self._inject = inject
         B = self.B if x0 is None else x0.shape[0]
+        HW = self.H * self.H
+        self.grad_numel = None if global_count is None else float(global_count) * HW / self.world
         sb = self._use(B)
         if x0 is not None:
             sb.x0.copy_(x0.reshape(B, self.H, self.H))
@@ -232,7 +253,7 @@ class Trainer:
         if self.ddp and self.broadcast_buffers:
             import torch.distributed as dist
             dist.broadcast(self.bnflat, 0, group=self.group)
-        if self.use_graph and inject is None and B == self.B:
+        if self.use_graph and inject is None and B == self.B and self.grad_numel is None:
             if self.graph is None:
                 self._body(_s())          # eager warm-up step (loads every kernel) then capture
                 self._capture()
@@ -242,6 +263,39 @@ class Trainer:
             self._body(_s())
         self.steps += 1
         return self.loss
+
+
+def shard_epoch(order: torch.Tensor, batch_size: int, world: int, rank: int):
+    """Data-parallel batches of one epoch for ``rank``: [(indices, global_count)], the same count of steps on
+    every rank (a rank that ran an extra step would wait forever in its all-reduce).
+
+    Global step j takes order[j*G : (j+1)*G] with G = batch_size * world (the reference's loop over one shuffled
+    epoch, code/train_diffusion_condition.py:214-216, at a global batch of G) and splits it into ``world``
+    contiguous near-equal parts (sizes differ by at most one).  ``global_count`` is that step's global batch size,
+    passed to Trainer.step so the gradient is the mean over all its samples (each rank weighted by its sample
+    count).  A last global batch with fewer samples than ranks is skipped (at most world - 1 samples of an epoch;
+    the permutation differs every epoch)."""
+    G = batch_size * world
+    out = []
+    for j in range(0, len(order), G):
+        part = order[j:j + G]
+        R = len(part)
+        if R < world:
+            break
+        lo = rank * (R // world) + min(rank, R % world)
+        n = R // world + (1 if rank < R % world else 0)
+        out.append((part[lo:lo + n], R))
+    return out
+
+
+def adam_bias_table(beta1: float, beta2: float, n: int = 40960) -> torch.Tensor:
+    """[n, 2] fp64: 1 - beta1**step and (1 - beta2**step)**0.5 for step = 1..n, evaluated with the Python-float
+    expressions of torch.optim.Adam (_single_tensor_adam), so the device step size equals torch's bit for bit.
+    The last row must be exactly (1, 1): later steps reuse it (both powers are below 2^-54 by then)."""
+    rows = [(1 - beta1 ** float(s), (1 - beta2 ** float(s)) ** 0.5) for s in range(1, n + 1)]
+    if rows[-1] != (1.0, 1.0):
+        raise ValueError("bias-correction table too short for these betas")
+    return torch.tensor(rows, dtype=torch.float64)
 
 
 class _StepBufs:

@@ -212,16 +212,21 @@ int cdm_perturb(const float* x, const float* noise, const int* t, const int* cur
  * acc[n] += (mean (pred - noise)^2 * mul[i]) / div[i], i = t[n] or *cur_i (noise row (T - i)*nstride) */
 int cdm_mse_accum(const float* pred, const float* noise, long long nstride, int T, int N, int HW, const int* t,
                   const int* cur_i, const float* mul, const float* div, float* acc, void* stream);
-/* F.mse_loss + its gradient (code/train_diffusion_condition.py:227) */
-int cdm_mse(const float* pred, const float* noise, long long n, float* dpred, float* partial, int nb, float* loss_out,
-            float* dbias_out, void* stream);
+/* F.mse_loss + its gradient (code/train_diffusion_condition.py:227): loss = mean over the n elements, dpred =
+ * 2 (pred - noise) / grad_numel (grad_numel = n, or the data-parallel count of a ragged global batch);
+ * nonfinite (optional): += 1 when the loss is NaN / inf (SURVEY §5 failure guard; read once per epoch) */
+int cdm_mse(const float* pred, const float* noise, long long n, double grad_numel, float* dpred, float* partial, int nb,
+            float* loss_out, float* dbias_out, int* nonfinite, void* stream);
 /* sampler: per-step prologue (device step counter) and denoise_add_noise + CFG combine
  * (code/train_diffusion_condition.py:274-279, 312-333) */
 int cdm_sample_prologue(int* ctr, int T, int* cur_i, float* t_cur, const float* sc_table, int sc_row, float* sc_cur,
                         void* stream);
+/* z: z_table[(T - i) * zstride + e] when given, else Philox keyed by seed ^ *seed_dev (seed_dev optional: a
+ * per-run device value, so one captured graph draws a fresh z sequence on every run) */
 int cdm_denoise(const float* xin, float* x, float* x2, long long numel, const float* eps, int cfg, float w,
                 const int* cur_i, const float* coef, const float* sa, const float* sb, const float* z_table,
-                long long zstride, unsigned long long seed, const int* snap_slot, float* snaps, int T, void* stream);
+                long long zstride, unsigned long long seed, const long long* seed_dev, const int* snap_slot,
+                float* snaps, int T, void* stream);
 /* randn_like / randint / the per-forward random 1x1 shortcut draw (diffusion_utilities.py:54), on-device Philox.
  * The stream id is sub (+ *sub_dev when given: a device counter advanced by cdm_counter_add, so a captured
  * step draws fresh numbers on every replay). */
@@ -232,9 +237,12 @@ int cdm_philox_uniform(float* out, long long n, float lo, float hi, unsigned lon
 int cdm_philox_randint(int* out, int n, int lo, int hi, unsigned long long seed, unsigned int sub, const int* sub_dev,
                        void* stream);
 int cdm_counter_add(int* ctr, int delta, void* stream);
-/* torch.optim.Adam step (code/train_diffusion_condition.py:200,229); state = {lr, step, -, -} in device memory */
-int cdm_adam(float* p, const float* g, float* m, float* v, long long n, float* state, double beta1, double beta2,
-             double eps, float grad_scale, void* stream);
+/* torch.optim.Adam step (code/train_diffusion_condition.py:200,229) with torch's CPU roundings.
+ * state (double[4], device) = {lr, step count, scratch, scratch}; bc (double[nbc][2], device) = host-evaluated
+ * {1 - beta1**s, (1 - beta2**s)**0.5} for s = 1..nbc (steps past nbc reuse the last row, which must be {1, 1}).
+ * grad_scale multiplies g (1/world for a summed data-parallel gradient). */
+int cdm_adam(float* p, const float* g, float* m, float* v, long long n, double* state, const double* bc, int nbc,
+             double beta1, double beta2, double eps, float grad_scale, void* stream);
 /* weight repacking (+ eval-mode BatchNorm folding) */
 /* kc = 0: K order tap-major (k = tap*C + ci); kc = 16: channel-chunk-major (k = ((ci/16)*9 + tap)*16 + ci%16),
  * the order cdm_conv3x3_fwd(kc = 16) consumes (wdg is chunked over Cout).  ConvTranspose packing: */

@@ -356,7 +356,7 @@ def test_split_f16x2_terms(L):
 
 
 @pytest.mark.parametrize("N,S,C,Cin", [(2, 64, 128, 128), (2, 32, 256, 128), (1, 32, 128, 256), (2, 32, 256, 256),
-                                       (1, 128, 256, 128)])
+                                       (1, 128, 256, 128), (256, 64, 128, 128), (256, 32, 256, 256)])
 def test_bn_bwd_fused_into_conv_staging_bit_exact(L, N, S, C, Cin):
     """Fused BN backward (dy computed while staging, never written) == norm_apply_bwd mode 0 then the h3
     convs, bit for bit: dgrad (LDS-halo kernel) and wgrad (kernel-row kernel) at the same operand scale; the
@@ -429,3 +429,60 @@ def test_halo_conv_tiles_per_block_bit_exact(L, N, tpb):
     torch.cuda.synchronize()
     assert torch.isfinite(ref).all()
     assert torch.equal(got, ref)
+
+
+def test_conv3x3_h3_bench_launch_shape(L):
+    """The C2 bench launch itself: N=256, 64x64, 128 -> 128 (4,096 256-pixel tiles, multi-tile blocks and the XCD
+    remap of the LDS-halo kernel, split-K over 1 M pixels in the weight gradient) — fwd with the bias / BN-stats /
+    max|y| epilogue, dgrad, wgrad against torch CPU (fp32 for fwd / dgrad at the 2e-5 bar; the weight gradient
+    against an fp64 GEMM over all 1,048,576 pixels at 5e-5)."""
+    from cdm_amd.engine import wgrad_splits
+    N, H, C = 256, 64, 128
+    P = N * H * H
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(N, C, H, H, generator=g).relu_()
+    W = torch.randn(C, C, 3, 3, generator=g) * 0.05
+    b = torch.randn(C, generator=g)
+    gy = torch.randn(N, C, H, H, generator=g) * 1e-3
+    Wc, bc = W.cuda(), b.cuda()
+    wpk, wdg = _pack3x3(L, Wc, bc, 16)
+    (wx, amw), (wdx, amd) = _split_h3(L, wpk, 9 * C, C), _split_h3(L, wdg, 9 * C, C)
+    xn, gyn = _nhwc(x), _nhwc(gy)
+    amx, amg = _amax(L, xn, P, C), _amax(L, gyn, P, C)
+    y = torch.empty(P, C, device="cuda")
+    stats = torch.zeros((P + 127) // 128, 2, C, device="cuda")
+    amy = torch.zeros(1, device="cuda")
+    L.cdm_conv3x3_fwd_h3(xn.data_ptr(), N, H, H, C, C, wx.data_ptr(), amx.data_ptr(), amw.data_ptr(), bc.data_ptr(),
+                         y.data_ptr(), C, C, 0, stats.data_ptr(), C, 16, amy.data_ptr(), _s())
+    dx = torch.empty(P, C, device="cuda")
+    L.cdm_conv3x3_fwd_h3(gyn.data_ptr(), N, H, H, C, C, wdx.data_ptr(), amg.data_ptr(), amd.data_ptr(), None,
+                         dx.data_ptr(), C, C, 0, None, 0, 16, None, _s())
+    sp = wgrad_splits(P, C, 9 * C)
+    slab = torch.full((sp, C, 9 * C), float("nan"), device="cuda")
+    L.cdm_conv3x3_wgrad_h3(gyn.data_ptr(), C, C, xn.data_ptr(), N, H, H, C, C, amg.data_ptr(), amx.data_ptr(), sp,
+                           slab.data_ptr(), _s())
+    dW = torch.empty(C, C, 3, 3, device="cuda")
+    L.cdm_slab_reduce(slab.data_ptr(), sp, C, 9 * C, dW.data_ptr(), 9 * C, 1, 9, C, 0, 1.0, _s())
+    torch.cuda.synchronize()
+    yc = y.cpu()
+    assert amy.item() == yc.abs().max().item()
+    with torch.no_grad():
+        ref = F.conv2d(x, W, b, padding=1)                       # torch CPU fp32
+        _close(yc.reshape(N, H, H, C).permute(0, 3, 1, 2), ref)
+        yr = ref.permute(0, 2, 3, 1).reshape(P, C).double()
+        st = stats.cpu().double().sum(0)
+        _close(st[0], yr.sum(0), 1e-4)
+        _close(st[1], (yr ** 2).sum(0), 1e-4)
+        del ref, yr
+        dref = torch.nn.grad.conv2d_input(x.shape, W, gy, padding=1)
+        _close(_nchw(dx, N, H, H, C), dref)
+        del dref
+        # weight gradient in fp64: dW[co][ci][ky][kx] = sum_p gy[p][co] * x[p + (ky-1, kx-1)][ci]
+        gyd = gy.permute(0, 2, 3, 1).reshape(P, C).double()
+        xp = F.pad(x, (1, 1, 1, 1)).permute(0, 2, 3, 1).double()
+        wref = torch.empty(C, C, 3, 3, dtype=torch.float64)
+        for ky in range(3):
+            for kx in range(3):
+                xs = xp[:, ky:ky + H, kx:kx + H, :].reshape(P, C)
+                wref[:, :, ky, kx] = gyd.t() @ xs
+        _close(dW, wref.float(), 5e-5)

@@ -168,3 +168,41 @@ def test_batch_elbo_bit_exact(golden_dir):
     e, bp = R.calculate_elbo_and_bpd_batch(g("batch_x"), g("batch_pred"), g("batch_noise"), g("batch_t"), b, a, ab,
                                            64 * 64)
     assert e.item() == float(lfx["batch_elbo"]) and bp.item() == float(lfx["batch_bpd"])
+
+
+def test_train_loop_with_lr_decay_bit_exact(golden_dir):
+    """train_nf8.npz (make_golden_r2.py): three reference loop iterations incl. the per-epoch LR change — the
+    oracle's OracleTrainer reproduces every post-step state_dict (parameters, BN buffers) bit for bit."""
+    fx = np.load(os.path.join(golden_dir, "train_nf8.npz"))
+    base = np.load(os.path.join(golden_dir, "model_nf8.npz"))
+    sd = {k[3:]: torch.from_numpy(base[k].copy()) for k in base.files if k.startswith("sd.")}
+    T = int(fx["T"])
+    _, _, ab = R.make_schedule(T)
+    tr = R.OracleTrainer(sd, n_feat=8, n_cfeat=6, height=64, lr=float(fx["lrate"]))
+    x, c = torch.from_numpy(fx["x"]), torch.from_numpy(fx["c"])
+    for k in range(3):
+        w = torch.from_numpy(fx[f"s{k}_sc_w"]).reshape(8, 1, 1, 1)
+        b = torch.from_numpy(fx[f"s{k}_sc_b"])
+        loss, _, g = tr.step(x, c, torch.from_numpy(fx[f"s{k}_noise"]), torch.from_numpy(fx[f"s{k}_t"]), T, ab, (w, b),
+                             lr=float(fx[f"s{k}_lr"]))
+        assert float(loss) == float(fx[f"s{k}_loss"])
+        if k == 0:
+            for n, v in g.items():
+                assert np.array_equal(v.numpy(), fx["s0_grad." + n]), n
+        for n, v in tr.sd.items():
+            assert np.array_equal(v.detach().numpy(), fx[f"s{k}_after.{n}"]), (k, n)
+    assert [float(fx[f"s{k}_lr"]) for k in range(3)] == [1e-3, 1e-3, 7.5e-4]
+
+
+def test_sampler_T1500_bit_exact(golden_dir):
+    """sampler_T1500_nf8.npz, w=0: the oracle's sample_loop replays the reference's 1500-step CPU run bit for bit
+    (x_T, 1499 z and 1500 shortcut draws from the CPU RNG)."""
+    fx = np.load(os.path.join(golden_dir, "sampler_T1500_nf8.npz"))
+    base = np.load(os.path.join(golden_dir, "model_nf8.npz"))
+    sd = {k[3:]: torch.from_numpy(base[k].copy()) for k in base.files if k.startswith("sd.")}
+    T = int(fx["T"])
+    torch.manual_seed(int(fx["w0_seed"]))
+    fn = R.make_model_fn(sd, n_feat=8, n_cfeat=6, height=64)
+    x, inter = R.sample_ddpm(fn, 2, 64, torch.from_numpy(fx["params"]), 0.0, T, R.make_schedule(T), 6)
+    assert np.array_equal(x.numpy(), fx["w0_x"])
+    assert np.array_equal(inter.numpy()[list(fx["snap_keep"])], fx["w0_inter"])
