@@ -20,6 +20,10 @@ static __device__ __forceinline__ float f4get(const float4& v, int j) {
     return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
 }
 
+// ReLU with torch's NaN semantics (torch.relu(nan) = nan; fmaxf would return 0 and hide a diverged step from the
+// trainer's non-finite-loss guard)
+static __device__ __forceinline__ float relu_f(float x) { return x < 0.f ? 0.f : x; }
+
 // exact (erf) GELU, as torch.nn.GELU() default (diffusion_utilities.py:130, ContextUnet.py:17)
 static __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 static __device__ __forceinline__ float gelu_grad_f(float x) {

@@ -197,7 +197,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
             CDM_FOR_ACC({
                 float v = acc[i][j][r] + bj[j];
                 if (accum) v += yz[(long long)m * ldy + n];
-                if (relu) v = fmaxf(v, 0.f);
+                if (relu) v = relu_f(v);
                 yz[(long long)m * ldy + n] = v;
                 cs[j] += v; cq[j] += v * v;
                 am = fmaxf(am, fabsf(v));
@@ -209,7 +209,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
                     if (bias) v += bias[n % bias_mod];
                     float* p = yz + (long long)m * ldy + n;
                     if (flags & EPI_ACCUM) v += *p;
-                    if (flags & EPI_RELU) v = fmaxf(v, 0.f);
+                    if (flags & EPI_RELU) v = relu_f(v);
                     *p = v;
                     cs[j] += v; cq[j] += v * v;
                     am = fmaxf(am, fabsf(v));
@@ -1911,16 +1911,29 @@ CDM_API int cdm_split_f16x2(const float* b, long long ldb, int K, int N, const f
     return cdm_status();
 }
 
-CDM_API int cdm_zero_f32(float* p, long long n, void* stream) {
-    return n > 0 ? (int)hipMemsetAsync(p, 0, (size_t)n * sizeof(float), S(stream)) : 0;
+// A kernel, not hipMemsetAsync: on this ROCm a memset captured into a hipGraph did not reliably clear its buffer on
+// later replays (tools/graph_probe.py: a 192-float memset node replayed after the buffer was rewritten left
+// garbage), which made replayed sampling steps inherit stale h3 operand maxima.  Every clear on a captured path
+// goes through this kernel.
+__global__ void fill_f32_kernel(float* p, long long n, float v) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        p[i] = v;
 }
+static int fill_f32(float* p, long long n, float v, hipStream_t s) {
+    if (n <= 0) return 0;
+    long long blocks = (n + 255) / 256;
+    blocks = blocks > 4096 ? 4096 : blocks;
+    hipLaunchKernelGGL(fill_f32_kernel, dim3((int)blocks), dim3(256), 0, s, p, n, v);
+    return cdm_status();
+}
+CDM_API int cdm_zero_f32(float* p, long long n, void* stream) { return fill_f32(p, n, 0.f, S(stream)); }
 
 CDM_API int cdm_amax_f32(const float* x, long long rows, int C, long long ld, float* out, int accumulate,
                          void* stream) {
     if (rows < 0 || C < 0 || ld < C) return (int)hipErrorInvalidValue;
     if (!accumulate) {
-        const hipError_t e = hipMemsetAsync(out, 0, sizeof(float), S(stream));
-        if (e != hipSuccess) return (int)e;
+        const int e = fill_f32(out, 1, 0.f, S(stream));
+        if (e) return e;
     }
     const long long total = rows * (long long)C;
     if (total == 0) return 0;

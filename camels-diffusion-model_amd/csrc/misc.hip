@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void conv_cin1_fwd_kernel(const float* x, int 
         }
         if (relu) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = fmaxf(o[j], 0.f);
+            for (int j = 0; j < 4; ++j) o[j] = relu_f(o[j]);
         }
         st4(y + pix * ldy + c4, make_float4(o[0], o[1], o[2], o[3]));
     }

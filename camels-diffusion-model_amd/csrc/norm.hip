@@ -78,7 +78,7 @@ struct NormBwdF {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     norm_elem(np, n, c, f4get(yv[e], j), zp[e], xh[e]);
-                    const float z = fmaxf(zp[e], 0.f);
+                    const float z = relu_f(zp[e]);
                     if (z > best || isnan(z)) { best = z; arg = e; }
                 }
                 const float gj = f4get(gv, j);
@@ -97,7 +97,7 @@ struct NormBwdF {
                 float zp, xh; norm_elem(np, n, c, f4get(yv, j), zp, xh);
                 float gz = f4get(gv, j);
                 if constexpr (FILM) {
-                    const float u = fmaxf(zp, 0.f);
+                    const float u = relu_f(zp);
                     acc[2 * 4 + j] += gz * u; acc[3 * 4 + j] += gz;
                     gz *= fp.a[n * fp.an + c];
                 }
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) void norm_apply_fwd_kernel(const float* y, int
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     float z = f4get(v, j) * np.s[n * np.sn + c4 + j] + np.t[n * np.sn + c4 + j];
-                    if (RELU) z = fmaxf(z, 0.f);
+                    if (RELU) z = relu_f(z);
                     if (z > o[j] || isnan(z)) o[j] = z;
                 }
             }
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(256) void norm_apply_fwd_kernel(const float* y, int
             for (int j = 0; j < 4; ++j) {
                 const int c = c4 + j;
                 float z = f4get(v, j) * np.s[n * np.sn + c] + np.t[n * np.sn + c];
-                if (RELU) z = fmaxf(z, 0.f);
+                if (RELU) z = relu_f(z);
                 if constexpr (FILM) z = fp.a[n * fp.an + c] * z + fp.b[n * fp.bn + c];
                 if constexpr (RESID) {
                     const int sel = n >= rp.split ? C : 0;
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(256) void norm_apply_bwd_kernel(const float* g, int
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     norm_elem(np, n, c, f4get(yv[e], j), zp[e], xh[e]);
-                    const float z = fmaxf(zp[e], 0.f);
+                    const float z = relu_f(zp[e]);
                     if (z > best || isnan(z)) { best = z; arg = e; }
                 }
                 const float a = A[n * cn + c], b = B[n * cn + c], cc = Cc[n * cn + c];

@@ -231,13 +231,14 @@ class GraphSampler:
 
         Returns (x [n,1,H,H], intermediate np [slots,n,1,H,H] or None)."""
         n, H = self.n, self.H
+        if self.z_source == "device":
+            # fresh z for every run, drawn from torch's CUDA generator (the reference's randn_like(x) on the device
+            # consumes it too): reproducible under torch.cuda.manual_seed, different across consecutive calls.
+            # Drawn before prepare(): a graph capture moves the generator's offset.
+            self.zseed.random_()
         self.prepare()
         total = self.T if steps is None else min(int(steps), self.T)
         self.xbuf[:n] = x_T.to(self.dev, torch.float32).reshape(n, H, H)
-        if self.z_source == "device":
-            # fresh z for every run, drawn from torch's CUDA generator (the reference's randn_like(x) on the device
-            # consumes it too): reproducible under torch.cuda.manual_seed, different across consecutive calls
-            self.zseed.random_(generator=None)
         if self.cfg:
             self.xbuf[n:] = self.xbuf[:n]
         self.ctr.fill_(self.T)

@@ -206,14 +206,16 @@ class Trainer:
                        self.T, _p(sb.xpert), _p(sb.t_in), s)
         self.eng.repack(P, True, s)
         eps = self.eng.forward(sb.ws, P, sb.xpert, sb.t_in, sb.c, self.sc[:nf], self.sc[nf:], B, s)
-        lb.cdm_mse(_p(eps), _p(sb.noise), B * HW, _p(sb.deps), _p(self.partial), self.nb, _p(self.loss),
-                   _p(self.grads["out.3.bias"]), s)
-        hook = self.bucketer.stage_ready if self.ddp else None
+        gnum = float(B * HW) if self.grad_numel is None else float(self.grad_numel)
+        lb.cdm_mse(_p(eps), _p(sb.noise), B * HW, gnum, _p(sb.deps), _p(self.partial), self.nb, _p(self.loss),
+                   _p(self.grads["out.3.bias"]), _p(self.nonfinite), s)
+        hooks = [h for h in (self.bucketer.stage_ready if self.ddp else None, self.stage_hook) if h is not None]
+        hook = (lambda name: [h(name) for h in hooks]) if hooks else None
         self.eng.backward(sb.ws, P, sb.deps, self.grads, s, out3_bias_done=True, on_stage=hook)
         if self.ddp:
             self.bucketer.wait()
-        lb.cdm_adam(_p(self.flat), _p(self.gflat), _p(self.m), _p(self.v), self.total, _p(self.opt_state), 0.9, 0.999,
-                    1e-8, 1.0 / self.world, s)
+        lb.cdm_adam(_p(self.flat), _p(self.gflat), _p(self.m), _p(self.v), self.total, _p(self.opt_state),
+                    _p(self.adam_bc), self.adam_bc.shape[0], self.betas[0], self.betas[1], self.eps, 1.0 / self.world, s)
         lb.cdm_counter_add(_p(self.ctr), 1, s)
 
     def _rank(self):

@@ -102,7 +102,7 @@ int cdm_minmax_f32(const float* x, long long n, unsigned* keys, float* out, void
 /* dst[N][O][O] = bilinear(O x O, align_corners=False)((log10(shift(src) / max) - min) / (max - min)) of src[N][S][S],
  * with minmax = cdm_minmax_f32 of the whole raw dataset (every step of the reference is monotone) */
 int cdm_camels_maps(const float* src, int N, int S, int O, const float* minmax, float* dst, void* stream);
-/* p[0..n) = 0 (hipMemsetAsync; graph-capturable) */
+/* p[0..n) = 0 (a fill kernel: graph-capturable; a captured hipMemsetAsync did not clear reliably on replay) */
 int cdm_zero_f32(float* p, long long n, void* stream);
 /* Producers below (cdm_norm_apply_fwd / _bwd, cdm_convT2x2_fwd, cdm_conv3x3_fwd_h3 amax_y) take an optional
  * float* amax: when non-null they atomically max the |values| they store into it, so the next h3 conv gets

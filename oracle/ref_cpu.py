@@ -248,6 +248,29 @@ class OracleTrainer:
         return loss.detach(), pred.detach(), grads
 
 
+def adam_step_restated(p, g, m, v, lr, step, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.0):
+    """One torch.optim.Adam step (torch/optim/adam.py _single_tensor_adam, the reference's optimizer,
+    code/train_diffusion_condition.py:200,229) restated elementwise in numpy fp32 with the roundings of torch's
+    CPU kernels: lerp_ = fma(w, g - m, m); mul_(b2).addcmul_ = fma((1-b2) g, g, v b2); denom = sqrt(v) / bc2s + eps;
+    addcdiv_ = p + (-step_size * m) / denom; step_size / bc2s from Python-float bias corrections, cast to fp32.
+    sqrt is correctly rounded here (torch's vectorised CPU sqrt may differ by an ulp, host-dependently).  fma is
+    evaluated as an exact fp64 product plus an fp64 add, then rounded (a double rounding can differ from a true
+    fma on ~1e-9 of the inputs).  Returns (p, m, v) as new float32 arrays."""
+    import numpy as np
+    f32 = np.float32
+
+    def fma(a, b, c):
+        return (np.float64(a) * np.asarray(b, np.float64) + np.asarray(c, np.float64)).astype(f32)
+    gi = (np.asarray(g, f32) * f32(grad_scale)).astype(f32)
+    bc1 = 1 - beta1 ** float(step)
+    bc2s = f32((1 - beta2 ** float(step)) ** 0.5)
+    nss = f32(-(lr / bc1))
+    m = fma(f32(1 - beta1), (gi - m).astype(f32), m)
+    v = fma((f32(1 - beta2) * gi).astype(f32), gi, (np.asarray(v, f32) * f32(beta2)).astype(f32))
+    denom = (np.sqrt(v) / bc2s + f32(eps)).astype(f32)
+    return (np.asarray(p, f32) + ((nss * m).astype(f32) / denom).astype(f32)).astype(f32), m, v
+
+
 # ----------------------------------------------------------------------------------------------
 # a10 / a11: samplers (CFG), replaying the reference RNG order on the CPU generator
 # ----------------------------------------------------------------------------------------------
