@@ -24,6 +24,10 @@ static __device__ __forceinline__ float f4get(const float4& v, int j) {
 // trainer's non-finite-loss guard)
 static __device__ __forceinline__ float relu_f(float x) { return x < 0.f ? 0.f : x; }
 
+// float <-> int key with the same order (signed int compare): atomicMax / atomicMin of floats on an int slot
+static __device__ __forceinline__ int fkey(float f) { const int i = __float_as_int(f); return i >= 0 ? i : i ^ 0x7FFFFFFF; }
+static __device__ __forceinline__ float fkey_inv(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
+
 // exact (erf) GELU, as torch.nn.GELU() default (diffusion_utilities.py:130, ContextUnet.py:17)
 static __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 static __device__ __forceinline__ float gelu_grad_f(float x) {

@@ -180,11 +180,13 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
     float* stats; int stats_ld;  // stats[tile][0|1][stats_ld]: sum / sum of squares of the stored value
     int M, N;
     float* amax = nullptr;       // optional running max|stored value| (block_amax_commit)
-
+    int* ymm = nullptr;          // optional per-column max / min of the stored value, ordered-int keys (fkey):
+    int ymm_ld = 0;              //   ymm[n] (atomic max), ymm[ymm_ld + n] (atomic min); needs stats
     __device__ __forceinline__ void operator()(f32x16 (&acc)[2][2], int mw, int nw, int lane, int wm, int wn,
                                                float* scratch, int tid) const {
         float* yz = y + (long long)blockIdx.z * zstride;
         float cs[2] = {0.f, 0.f}, cq[2] = {0.f, 0.f};
+        float cmx[2] = {-INFINITY, -INFINITY}, cmn[2] = {INFINITY, INFINITY};
         float am = 0.f;
         if (mw - wm * 64 + WM * 64 <= M && (nw - wn * 64) + GBN <= N) {
             // whole block tile in range (the hot shapes): no per-element bounds branches, bias hoisted (one
@@ -201,6 +203,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
                 yz[(long long)m * ldy + n] = v;
                 cs[j] += v; cq[j] += v * v;
                 am = fmaxf(am, fabsf(v));
+                cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
             })
         } else {
             CDM_FOR_ACC({
@@ -213,6 +216,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
                     *p = v;
                     cs[j] += v; cq[j] += v * v;
                     am = fmaxf(am, fabsf(v));
+                    cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
                 }
             })
         }
@@ -237,6 +241,36 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
                 float* st = stats + (long long)((mw - wm * 64) / GBM + t) * 2 * stats_ld;
                 st[n] = scratch[(4 * t + 0) * GBN + c] + scratch[(4 * t + 2) * GBN + c];
                 st[stats_ld + n] = scratch[(4 * t + 1) * GBN + c] + scratch[(4 * t + 3) * GBN + c];
+            }
+        }
+        if (!ymm) return;
+        // column max / min over the block (the next layer's exact max|relu(y s + t)|, see bn_fwd_finalize)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            cmx[j] = fmaxf(cmx[j], __shfl_xor(cmx[j], 32, 64));
+            cmn[j] = fminf(cmn[j], __shfl_xor(cmn[j], 32, 64));
+        }
+        __syncthreads();
+        if (lane < 32) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int c = wn * 64 + 32 * j + lane;
+                scratch[wm * GBN + c] = cmx[j];
+                scratch[(WM + wm) * GBN + c] = cmn[j];
+            }
+        }
+        __syncthreads();
+        if (tid < GBN) {
+            const int n = blockIdx.y * GBN + tid;
+            if (n < N) {
+                float mx = scratch[tid], mn = scratch[WM * GBN + tid];
+#pragma unroll
+                for (int w = 1; w < WM; ++w) {
+                    mx = fmaxf(mx, scratch[w * GBN + tid]);
+                    mn = fminf(mn, scratch[(WM + w) * GBN + tid]);
+                }
+                atomicMax(ymm + n, fkey(mx));
+                atomicMin(ymm + ymm_ld + n, fkey(mn));
             }
         }
     }
@@ -756,12 +790,23 @@ template <class LD> struct ColK { template <int NT> using T = StageColK<LD, NT>;
 // Optional staging pre-op of a conv operand.  PreBnBwd: the operand is dy of a Conv -> BatchNorm -> ReLU layer,
 // computed while staging from the grad g of the ReLU output and the pre-norm activations y (bn_bwd_elem, the
 // expression of norm_apply_bwd_kernel): dy is never written to HBM (no 537 MB write + 2 reads per layer).
-struct PreNone { static constexpr bool on = false; };
+struct PreNone { static constexpr bool on = false; static constexpr int kind = 0; };
 struct PreBnBwd {
     static constexpr bool on = true;
+    static constexpr int kind = 1;
     const float* y; int ldy;   // pre-norm activations [pix][C]
     const float* p[7];         // per channel: scale s, shift t, mean, invstd, A, B, Cc
 };
+// PreBnRelu: the operand is z = relu(y s + t) of a Conv -> BatchNorm -> ReLU layer (train mode), computed while
+// staging from the layer's pre-norm output y: z is never written (the apply kernel's 537 MB write + read at 64^2).
+// Zero padding stays zero (only in-image pieces are transformed).  Same fmaf as norm_apply_fwd: bit-identical.
+struct PreBnRelu {
+    static constexpr bool on = false;
+    static constexpr int kind = 2;
+    const float* p[2];         // per input channel: scale s, shift t
+};
+static __device__ __forceinline__ float bn_relu_elem(float y, float s, float t) { return relu_f(fmaf(y, s, t)); }
+
 
 // ============================== LDS-halo conv3x3 on the split-bf16 matrix cores ==============================
 // conv3x3 (stride 1, pad 1) forward / dgrad for Cin % 16 == 0 (channel-chunk-major K, kc = 16) and image
@@ -820,9 +865,10 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     const int nchunks = Cin / 16, ngroups = nchunks * 3;
     const float sx = op_scale<NT>(amax_x);
     // BN-backward pre-op: the block's per-channel coefficients, staged once (Cin <= 256)
-    __shared__ __attribute__((aligned(16))) float bcs[PRE::on ? 7 * 256 : 4];
-    if constexpr (PRE::on) {
-        for (int i = tid; i < 7 * Cin; i += HTHREADS) {
+    constexpr int NCOEF = PRE::kind == 1 ? 7 : (PRE::kind == 2 ? 2 : 0);
+    __shared__ __attribute__((aligned(16))) float bcs[NCOEF ? NCOEF * 256 : 4];
+    if constexpr (NCOEF > 0) {
+        for (int i = tid; i < NCOEF * Cin; i += HTHREADS) {
             const int k = i / Cin;
             bcs[i] = pre.p[k][i - k * Cin];
         }
@@ -868,11 +914,11 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         }
     };
     auto store_halo = [&](__bf16* base, int cc) {
-        float cf[PRE::on ? 7 : 1][4];   // coefficients of this thread's 4 channels (q & 3 == tid & 3 for every j)
-        if constexpr (PRE::on) {
+        float cf[NCOEF ? NCOEF : 1][4];   // coefficients of this thread's 4 channels (q & 3 == tid & 3 for every j)
+        if constexpr (NCOEF > 0) {
             const int cb = cc * 16 + (tid & 3) * 4;
 #pragma unroll
-            for (int k = 0; k < 7; ++k) {
+            for (int k = 0; k < NCOEF; ++k) {
                 const float4 v = *reinterpret_cast<const float4*>(bcs + k * Cin + cb);
                 cf[k][0] = v.x; cf[k][1] = v.y; cf[k][2] = v.z; cf[k][3] = v.w;
             }
@@ -881,12 +927,17 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         for (int j = 0; j < HQ; ++j) {
             if (hdst[j] >= 0) {
                 float xv[4] = {hreg[j].x, hreg[j].y, hreg[j].z, hreg[j].w};
-                if constexpr (PRE::on) {
+                if constexpr (PRE::kind == 1) {
                     if (hsrc[j]) {
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
                             xv[e] = bn_bwd_elem(xv[e], f4get(yreg[j], e), cf[0][e], cf[1][e], cf[2][e], cf[3][e],
                                                 cf[4][e], cf[5][e], cf[6][e]);
+                    }
+                } else if constexpr (PRE::kind == 2) {
+                    if (hsrc[j]) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) xv[e] = bn_relu_elem(xv[e], cf[0][e], cf[1][e]);
                     }
                 }
                 __bf16 h[4], m[4], l[4];
@@ -1266,14 +1317,16 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
 // kx shift), so each dY fragment feeds 3 taps and X is staged once instead of three times (2.5x less LDS
 // traffic per MFMA than the per-tap kernel above).  8 waves = 2 (co) x 4 (ci), wave tile 64 co x 32 ci x 3
 // taps (6 accumulators).  Split-K over pixel ranges; writes slab[z][co][tap*Cin+ci] like the per-tap kernel.
-template <int NT, int KS = 1, class PRE = PreNone>   // KS: 16-pixel K steps per barrier (W % (16 KS) == 0);
+template <int NT, int KS = 1, class PRE = PreNone, class PX = PreNone>
+                                // KS: 16-pixel K steps per barrier (W % (16 KS) == 0);
                                 // KS = 2: 1.09x KS = 1 (KS = 4 needs 133 KB of LDS: the launch is refused)
                                 // PRE = PreBnBwd: dy computed from g (the dy argument) and y while staging
+                                // PX = PreBnRelu: X = relu(y s + t) computed from the previous layer's y (the x argument)
 __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __restrict__ dy, int lddy, int Cout,
                                                               const float* __restrict__ x, int H, int W, int Cin,
                                                               int ldx, int ktiles, int kt_per_split,
                                                               const float* amax_dy, const float* amax_x,
-                                                              float* __restrict__ slab, PRE pre) {
+                                                              float* __restrict__ slab, PRE pre, PX px) {
     constexpr int NS = XTerms<NT>::NS;
     constexpr int RA = 16 * KS, RB = RA + 2;          // image rows (pixels): dY, X with its halo
     constexpr int IA = RA * 128, IB = RB * 128;       // bf16 per term image
@@ -1306,6 +1359,12 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
     const int p0 = kt0 * RA;
     int pn = p0 / hw, ph = (p0 - pn * hw) / W, pw = p0 - pn * hw - ph * W;
     float4 ra[KS], rb[KS], rb1 = f4zero();
+    bool vb[KS], vb1 = false;       // PX: which X pieces lie inside the image (padding stays zero)
+    float xs[4], xt[4];             // PX coefficients of this thread's 4 input channels ci0 + c4
+    if constexpr (PX::kind == 2) {
+        const float4 a = ld4(px.p[0] + ci0 + c4), b = ld4(px.p[1] + ci0 + c4);
+        xs[0] = a.x; xs[1] = a.y; xs[2] = a.z; xs[3] = a.w; xt[0] = b.x; xt[1] = b.y; xt[2] = b.z; xt[3] = b.w;
+    }
     float4 ya[PRE::on ? KS : 1];
     float cf[PRE::on ? 7 : 1][4];   // PreBnBwd coefficients of this thread's 4 output channels m0 + c4
     if constexpr (PRE::on) {
@@ -1325,14 +1384,24 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
             ra[k] = ld4(dy + pix * lddy + m0 + c4);
             if constexpr (PRE::on) ya[k] = ld4(pre.y + pix * pre.ldy + m0 + c4);
             const int w0 = pw - 1 + sr + 16 * k;
-            rb[k] = (rowok && (unsigned)w0 < (unsigned)W) ? ld4(x + (xrow + w0) * ldx + ci0 + c4) : f4zero();
+            vb[k] = rowok && (unsigned)w0 < (unsigned)W;
+            rb[k] = vb[k] ? ld4(x + (xrow + w0) * ldx + ci0 + c4) : f4zero();
         }
         if (tid < 64) {
             const int w1 = pw + RA - 1 + sr;
-            rb1 = (rowok && w1 < W) ? ld4(x + (xrow + w1) * ldx + ci0 + c4) : f4zero();
+            vb1 = rowok && w1 < W;
+            rb1 = vb1 ? ld4(x + (xrow + w1) * ldx + ci0 + c4) : f4zero();
         }
         pw += RA;
         if (pw >= W) { pw = 0; if (++ph == H) { ph = 0; ++pn; } }
+    };
+    auto xpre = [&](const float4& v, bool valid) -> float4 {   // PX transform at staging time (after the load wait)
+        if constexpr (PX::kind == 2) {
+            if (valid)
+                return make_float4(bn_relu_elem(v.x, xs[0], xt[0]), bn_relu_elem(v.y, xs[1], xt[1]),
+                                   bn_relu_elem(v.z, xs[2], xt[2]), bn_relu_elem(v.w, xs[3], xt[3]));
+        }
+        return v;
     };
     auto put = [&](char* img, int row, const float4& v, float sc, int ielems) {
         const float xv[4] = {v.x, v.y, v.z, v.w};
@@ -1359,9 +1428,9 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
             } else {
                 put(a, sr + 16 * k, ra[k], sa, IA);
             }
-            put(b, sr + 16 * k, rb[k], sb, IB);
+            put(b, sr + 16 * k, xpre(rb[k], vb[k]), sb, IB);
         }
-        if (tid < 64) put(b, RA + sr, rb1, sb, IB);
+        if (tid < 64) put(b, RA + sr, xpre(rb1, vb1), sb, IB);
     };
     // transposed-read addresses (see the per-tap kernel); tap t reads X rows shifted by t
     const int g = (lane >> 4) & 3, q = (lane >> 2) & 3, pq = lane & 3;
@@ -1543,6 +1612,56 @@ __global__ void split_f16x2_kernel(const float* __restrict__ b, long long ldb, i
     }
 }
 
+// ---- batched train-mode weight repack of every 3x3 conv (one amax launch + one pack-and-split launch per step
+//      instead of ~7 small launches per layer): OIHW W -> the h3 split images the halo conv reads, directly ----
+struct PackSplitJob {
+    const float* W;          // OIHW [Cout][Cin][3][3]
+    int Cin, Cout, kc;       // kc: K order (16 = channel-chunk-major, 0 = tap-major), as cdm_pack_conv3x3
+    int pad_;
+    __bf16* wpk_x;           // fwd operand  [ceil(9 Cin / 16)][3][Cout][16]  (K = tap/ci, N = co)
+    __bf16* wdg_x;           // dgrad operand [ceil(9 Cout / 16)][3][Cin][16] (K = tap'/co, N = ci), W flipped
+    float* amax;             // max|W| (the split scale of both images)
+};
+static __device__ __forceinline__ void unk(int k, int C, int kc, int& tap, int& c) {   // inverse of kidx
+    if (kc <= 0) { tap = k / C; c = k - tap * C; return; }
+    const int cc = k / (9 * kc), rem = k - cc * 9 * kc;
+    tap = rem / kc; c = cc * kc + (rem - tap * kc);
+}
+__global__ __launch_bounds__(256) void pack_amax_batch_kernel(const PackSplitJob* __restrict__ jobs) {
+    const PackSplitJob j = jobs[blockIdx.y];
+    const long long total = (long long)j.Cout * j.Cin * 9;
+    float m = 0.f;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
+        m = fmaxf(m, fabsf(j.W[i]));
+    block_amax_commit(m, j.amax);
+}
+__global__ __launch_bounds__(256) void pack_split_batch_kernel(const PackSplitJob* __restrict__ jobs) {
+    const PackSplitJob j = jobs[blockIdx.y >> 1];
+    const bool dg = blockIdx.y & 1;
+    __bf16* out = dg ? j.wdg_x : j.wpk_x;
+    if (!out) return;
+    const int K = 9 * (dg ? j.Cout : j.Cin), N = dg ? j.Cin : j.Cout;
+    const float sc = op_scale<NT_H3>(j.amax);
+    const int ktiles = (K + XBK - 1) / XBK;
+    const long long total = (long long)ktiles * N * XBK;
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long long)gridDim.x * blockDim.x) {
+        const int kk = (int)(q % XBK); const long long r = q / XBK;
+        const int n = (int)(r % N); const int kt = (int)(r / N);
+        const int k = kt * XBK + kk;
+        float v = 0.f;
+        if (k < K) {
+            int tap, c;
+            if (!dg) { unk(k, j.Cin, j.kc, tap, c); v = j.W[((long long)n * j.Cin + c) * 9 + tap]; }          // W[co=n][ci=c]
+            else     { unk(k, j.Cout, j.kc, tap, c); v = j.W[((long long)c * j.Cin + n) * 9 + (8 - tap)]; }  // W[co=c][ci=n]
+        }
+        v *= sc;
+        const _Float16 h = (_Float16)v;
+        __bf16* o = out + (((long long)kt * 3) * N + n) * XBK + kk;
+        o[0] = __builtin_bit_cast(__bf16, h);
+        o[(long long)N * XBK] = __builtin_bit_cast(__bf16, (_Float16)(v - (float)h));
+    }
+}
+
 // out = max(out, max |x[r*ld + c]|) over r < rows, c < C  (atomic max on the float's bits; NaN ignored)
 __global__ void amax_kernel(const float* __restrict__ x, long long rows, int C, long long ld, unsigned* out) {
     float m = 0.f;
@@ -1698,14 +1817,22 @@ CDM_API int cdm_conv3x3_fwd_variant(int variant, const float* x, int N, int H, i
 // wx = the split packed weights (cdm_split_bf16x3 / cdm_split_f16x2, same K order kc as cdm_pack_conv3x3).
 static int conv3x3_fwd_split(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
                              const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags,
-                             float* stats, int stats_ld, int kc, int nterm, float* amax_y, hipStream_t st) {
+                             float* stats, int stats_ld, int kc, int nterm, float* amax_y, hipStream_t st,
+                             const float* pre_s = nullptr, const float* pre_t = nullptr, int* ymm = nullptr,
+                             int ymm_ld = 0) {
     if (Cin % 4 || Cout % 4 || (kc != 0 && kc != 16) || (kc == 16 && Cin % 16)) return (int)hipErrorInvalidValue;
     const int M = N * H * W, K = 9 * Cin;
     MkPre mb{reinterpret_cast<const __bf16*>(wx), Cout, amax_w};
     EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
-    if (kc == 16 && W == H && halo_width_ok(W, nterm) && ldx % 4 == 0 && (H * W) % HBM_ == 0) {   // LDS-halo path
-        const EpiStoreW<4> eh{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
+    const bool halo = kc == 16 && W == H && halo_width_ok(W, nterm) && ldx % 4 == 0 && (H * W) % HBM_ == 0;
+    if ((pre_s || ymm) && (!halo || (ymm && !stats) || (pre_s && (!pre_t || Cin > 256))))
+        return (int)hipErrorInvalidValue;      // the fused BN-ReLU input / max-min epilogue: LDS-halo path only
+    if (halo) {   // LDS-halo path
+        EpiStoreW<4> eh{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
+        eh.ymm = ymm; eh.ymm_ld = ymm_ld;
         const __bf16* b = reinterpret_cast<const __bf16*>(wx);
+        if (pre_s) return launch_conv_halo_w(W, x, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st,
+                                             PreBnRelu{{pre_s, pre_t}});
         return launch_conv_halo_w(W, x, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st);
     }
     if (Cin == 128 && Cout == 128 && H == 64 && W == 64 && kc == 16) {
@@ -1794,21 +1921,41 @@ CDM_API int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int
                              NT_H3, amax_y, S(stream));
 }
 
-template <int KS, class PRE = PreNone>
+// cdm_conv3x3_fwd_h3 + two fusions of the train-mode Conv -> BatchNorm -> ReLU chain (LDS-halo path only):
+//   pre_s / pre_t (optional): the input is relu(x * pre_s[c] + pre_t[c]) of the previous layer's pre-norm output x
+//                             (its BN apply runs in this conv's staging; *amax_x must bound that z)
+//   ymm (optional, needs stats): per output channel max / min of y as ordered-int keys, ymm[c] / ymm[ymm_ld + c]
+//                             (cleared by the caller to INT_MIN / INT_MAX), for the next layer's exact max|z|
+CDM_API int cdm_conv3x3_fwd_h3_ex(const float* x, int N, int H, int W, int Cin, int ldx, const float* pre_s,
+                                  const float* pre_t, const void* wx, const float* amax_x, const float* amax_w,
+                                  const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
+                                  int kc, float* amax_y, int* ymm, int ymm_ld, void* stream) {
+    if (!amax_x || !amax_w) return (int)hipErrorInvalidValue;
+    return conv3x3_fwd_split(x, N, H, W, Cin, ldx, wx, amax_x, amax_w, bias, y, ldy, Cout, flags, stats, stats_ld, kc,
+                             NT_H3, amax_y, S(stream), pre_s, pre_t, ymm, ymm_ld);
+}
+
+template <int KS, class PRE = PreNone, class PX = PreNone>
 static int launch_wgrad_row(const float* dy, int lddy, int Cout, const float* x, int H, int W, int Cin, int ldx, int K,
                             int sp, const float* amax_dy, const float* amax_x, float* slab, int nterm, hipStream_t st,
-                            PRE pre = PRE{}) {
+                            PRE pre = PRE{}, PX px = PX{}) {
     const int ktiles = K / (16 * KS), per = (ktiles + sp - 1) / sp;
     dim3 grid((Cout / 128) * 3 * (Cin / 128) * ((ktiles + per - 1) / per));
+    if constexpr (PX::kind != 0) {            // the fused X transform is instantiated for the h3 arithmetic only
+        if (nterm != NT_H3) return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL((wgrad3x3_row_kernel<NT_H3, KS, PRE, PX>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W,
+                           Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px);
+        return cdm_status();
+    }
     switch (nterm) {
         case 1: hipLaunchKernelGGL((wgrad3x3_row_kernel<1, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
-                                   ktiles, per, amax_dy, amax_x, slab, pre); break;
+                                   ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}); break;
         case 3: hipLaunchKernelGGL((wgrad3x3_row_kernel<3, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
-                                   ktiles, per, amax_dy, amax_x, slab, pre); break;
+                                   ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}); break;
         case NT_H3: hipLaunchKernelGGL((wgrad3x3_row_kernel<NT_H3, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W,
-                                       Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre); break;
+                                       Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}); break;
         case 6: hipLaunchKernelGGL((wgrad3x3_row_kernel<6, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
-                                   ktiles, per, amax_dy, amax_x, slab, pre); break;
+                                   ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}); break;
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();
@@ -1892,6 +2039,32 @@ CDM_API int cdm_conv3x3_wgrad_h3_bnbwd(const float* g, int ldg, const float* y, 
     return (int)hipErrorInvalidValue;
 }
 
+// the kernel-row weight gradient with both staging fusions selectable: g / y / BN coefficients (optional, all or
+// none: the dY operand is the BN backward of g, as cdm_conv3x3_wgrad_h3_bnbwd) and x_s / x_t (optional: the X operand
+// is relu(x * x_s[c] + x_t[c]) of the previous layer's pre-norm output).  Cin % 128 == Cout % 128 == 0, W % 16 == 0.
+CDM_API int cdm_conv3x3_wgrad_h3_ex(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
+                                    const float* mean, const float* invstd, const float* A, const float* B,
+                                    const float* Cc, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,
+                                    const float* x_s, const float* x_t, const float* amax_dy, const float* amax_x,
+                                    int splits, float* slab, void* stream) {
+    if (Cin % 128 || Cout % 128 || W % 16 || ldg % 4 || ldx % 4 || !amax_dy || !amax_x || (x_s && !x_t) ||
+        (y && ldy % 4))
+        return (int)hipErrorInvalidValue;
+    const int K = N * H * W, sp = effective_splits(K, splits);
+    const bool ks2 = W % 32 == 0 && effective_splits(K, splits, 32) == sp;
+    if (!ks2 && effective_splits(K, splits, 16) != sp) return (int)hipErrorInvalidValue;
+    const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
+    const PreBnRelu px{{x_s, x_t}};
+    hipStream_t st = S(stream);
+#define CDM_WG(KS_, PRE_, PX_) launch_wgrad_row<KS_>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, \
+                                                     NT_H3, st, PRE_, PX_)
+    if (y && x_s) return ks2 ? CDM_WG(2, pre, px) : CDM_WG(1, pre, px);
+    if (y) return ks2 ? CDM_WG(2, pre, PreNone{}) : CDM_WG(1, pre, PreNone{});
+    if (x_s) return ks2 ? CDM_WG(2, PreNone{}, px) : CDM_WG(1, PreNone{}, px);
+    return ks2 ? CDM_WG(2, PreNone{}, PreNone{}) : CDM_WG(1, PreNone{}, PreNone{});
+#undef CDM_WG
+}
+
 static int split_blocks(int K, int N) {
     const long long total = (long long)((K + XBK - 1) / XBK) * N * XBK;
     long long blocks = (total + 255) / 256;
@@ -1927,6 +2100,21 @@ static int fill_f32(float* p, long long n, float v, hipStream_t s) {
     return cdm_status();
 }
 CDM_API int cdm_zero_f32(float* p, long long n, void* stream) { return fill_f32(p, n, 0.f, S(stream)); }
+
+/* every 3x3 conv's train-mode weight images in two launches: max|W| per job (into job.amax, cleared first by the
+   caller, e.g. cdm_zero_f32 over a slot array), then the h3 split images straight from OIHW W */
+CDM_API int cdm_pack_split_conv3x3_batch(const void* jobs_dev, int njobs, long long max_w_elems, void* stream) {
+    if (njobs <= 0 || njobs > 32768) return (int)hipErrorInvalidValue;
+    const PackSplitJob* jobs = reinterpret_cast<const PackSplitJob*>(jobs_dev);
+    long long bx = (max_w_elems + 255) / 256;
+    bx = bx > 64 ? 64 : (bx < 1 ? 1 : bx);
+    hipLaunchKernelGGL(pack_amax_batch_kernel, dim3((unsigned)bx, njobs), dim3(256), 0, S(stream), jobs);
+    int e = cdm_status(); if (e) return e;
+    long long sx = (max_w_elems * 3 / 2 + 255) / 256;       // split images pad K to 16: ~1 element per weight
+    sx = sx > 256 ? 256 : (sx < 1 ? 1 : sx);
+    hipLaunchKernelGGL(pack_split_batch_kernel, dim3((unsigned)sx, 2 * njobs), dim3(256), 0, S(stream), jobs);
+    return cdm_status();
+}
 
 CDM_API int cdm_amax_f32(const float* x, long long rows, int C, long long ld, float* out, int accumulate,
                          void* stream) {

@@ -160,15 +160,25 @@ __global__ __launch_bounds__(256) void conv_cin1_wgrad_kernel(const float* dy, i
 }
 
 // out[r*s_r + c*s_c] (+)= sum_s part[s][r0+r][c]  for r < rn   (part = fp64 partials of cdm_slab_colsum)
-__global__ void slab_sum_all_kernel(const double* part, int S, int R, int r0, int rn, int C, float* out,
-                                    long long s_r, long long s_c, int accumulate) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= rn * C) return;
-    const int r = idx / C, c = idx - r * C;
+// 64 outputs per block, the S partials split over the 4 waves and folded in a fixed order (deterministic)
+__global__ __launch_bounds__(256) void slab_sum_all_kernel(const double* part, int S, int R, int r0, int rn, int C,
+                                                           float* out, long long s_r, long long s_c, int accumulate) {
+    __shared__ double red[4][64];
+    const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6, idx = blockIdx.x * 64 + cl;
     double s = 0.0;
-    for (int t = 0; t < S; ++t) s += part[((long long)t * R + r0 + r) * C + c];
-    float* p = out + r * s_r + c * s_c;
-    *p = accumulate ? *p + (float)s : (float)s;
+    int r = 0, c = 0;
+    if (idx < rn * C) {
+        r = idx / C; c = idx - r * C;
+        const double* src = part + (long long)(r0 + r) * C + c;
+        for (int t = grp; t < S; t += 4) s += src[(long long)t * R * C];
+    }
+    red[grp][cl] = s;
+    __syncthreads();
+    if (grp == 0 && idx < rn * C) {
+        const double tot = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+        float* p = out + r * s_r + c * s_c;
+        *p = accumulate ? *p + (float)tot : (float)tot;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -321,6 +331,57 @@ __global__ __launch_bounds__(256) void conv_cout1_dgrad_kernel(const float* deps
             for (int j = 0; j < 4; ++j) o[j] = fmaf(g, wr[tap][j], o[j]);
         }
         st4(dz + pix * lddz + c4, make_float4(o[0], o[1], o[2], o[3]));
+    }
+}
+
+// out.3 weight gradient, band form: dW[c][tap] = sum_p deps[p] z[p + off_tap][c] = sum_q z[q][c] deps[q - off_tap].
+// A block owns R whole rows of one image; every z pixel q of the band is read from HBM once (float4 per lane,
+// C/4 lanes per pixel: one coalesced row), and its 9 contributions use the deps values around it, staged with a
+// zero border in LDS (no bounds tests).  Per-block partials [9][C] (fixed-order LDS fold over the pixel lanes).
+__global__ __launch_bounds__(256) void conv_cout1_wgrad_band_kernel(const float* __restrict__ deps,
+                                                                    const float* __restrict__ z, int ldz, int H, int W,
+                                                                    int C, int R, float* __restrict__ slab) {
+    extern __shared__ float sm[];                        // deps band [(R+2)][(W+2)], then the fold [PL][9][C]
+    const int bands = H / R, n = blockIdx.x / bands, h0 = (blockIdx.x - n * bands) * R;
+    const int C4 = C >> 2, PL = 256 / C4, tid = threadIdx.x, c4 = (tid % C4) * 4, pl = tid / C4;
+    const int DW = W + 2, DN = (R + 2) * DW;
+    float* dl = sm;
+    float* red = sm + ((DN + 3) & ~3);
+    for (int i = tid; i < DN; i += 256) {
+        const int rr = i / DW, cc = i - rr * DW, hh = h0 - 1 + rr, ww = cc - 1;
+        dl[i] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? deps[((long long)n * H + hh) * W + ww] : 0.f;
+    }
+    __syncthreads();
+    float acc[9][4];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[t][j] = 0.f;
+    if (pl < PL) {
+        const float* zb = z + ((long long)n * H + h0) * W * ldz + c4;
+        for (int q = pl; q < R * W; q += PL) {
+            const int r = q / W, c = q - r * W;
+            const float4 v = ld4(zb + (long long)q * ldz);
+            // output pixel p = q - off, off = (ky - 1, kx - 1): deps at band row r + 2 - ky, column c + 2 - kx
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    const float g = dl[(r + 2 - ky) * DW + (c + 2 - kx)];
+                    const int t = ky * 3 + kx;
+                    acc[t][0] = fmaf(g, v.x, acc[t][0]); acc[t][1] = fmaf(g, v.y, acc[t][1]);
+                    acc[t][2] = fmaf(g, v.z, acc[t][2]); acc[t][3] = fmaf(g, v.w, acc[t][3]);
+                }
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) st4(&red[(pl * 9 + t) * C + c4], make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]));
+    }
+    __syncthreads();
+    float* out = slab + (long long)blockIdx.x * 9 * C;
+    for (int idx = tid; idx < 9 * C; idx += 256) {
+        float s = 0.f;
+        for (int q = 0; q < PL; ++q) s += red[q * 9 * C + idx];
+        out[idx] = s;
     }
 }
 
@@ -731,7 +792,7 @@ CDM_API int cdm_conv3x3_cin1_wgrad(const float* dy, int lddy, const float* x, in
 }
 CDM_API int cdm_slab_sum_all(const double* part, int nparts, int R, int r0, int rn, int C, float* out, long long s_r,
                              long long s_c, int accumulate, void* stream) {
-    hipLaunchKernelGGL(slab_sum_all_kernel, dim3((rn * C + 255) / 256), dim3(256), 0, S(stream), part, nparts, R, r0, rn, C,
+    hipLaunchKernelGGL(slab_sum_all_kernel, dim3((rn * C + 63) / 64), dim3(256), 0, S(stream), part, nparts, R, r0, rn, C,
                        out, s_r, s_c, accumulate);
     return cdm_status();
 }
@@ -759,6 +820,14 @@ CDM_API int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int 
 CDM_API int cdm_conv3x3_cout1_wgrad(const float* deps, const float* z, int ldz, int N, int H, int W, int C, int csize,
                                     float* slab, void* stream) {
     if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
+    if (csize < 0) {                  // band form: R = -csize whole rows per block, partials [N * H / R][9][C]
+        const int R = -csize;
+        const size_t lds = (((size_t)(R + 2) * (W + 2) + 3) & ~(size_t)3) * 4 + (size_t)(256 / (C / 4)) * 9 * C * 4;
+        if (H % R || ldz % 4 || lds > 64 * 1024) return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL(conv_cout1_wgrad_band_kernel, dim3(N * (H / R)), dim3(256), lds, S(stream), deps, z, ldz, H,
+                           W, C, R, slab);
+        return cdm_status();
+    }
     hipLaunchKernelGGL(conv_cout1_wgrad_kernel, dim3((H * W + csize - 1) / csize, N), dim3(256), 0, S(stream), deps, z,
                        ldz, H, W, C, csize, slab);
     return cdm_status();

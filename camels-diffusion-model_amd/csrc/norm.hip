@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void slab_colsum_kernel(const float* __restric
 __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* part, int S, int R, int C, double count,
                                        const float* gamma, const float* beta, float* rmean, float* rvar,
                                        long long* nbt, float momentum, float eps, float* mean, float* invstd,
-                                       float* scale, float* shift) {
+                                       float* scale, float* shift, const int* ymm, int ymm_ld, float* amax_z) {
     __shared__ double rs[16][17], rq[16][17];
     const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
     const int c = blockIdx.x * 16 + cl;
@@ -201,7 +201,13 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* part
     const float is = (float)(1.0 / sqrt(var + (double)eps));
     mean[c] = (float)mu; invstd[c] = is;
     const float sc = gamma[c] * is;
-    scale[c] = sc; shift[c] = beta[c] - (float)mu * sc;
+    const float sh = beta[c] - (float)mu * sc;
+    scale[c] = sc; shift[c] = sh;
+    if (ymm) {   // exact max over the layer of z = relu(fmaf(y, sc, sh)): monotone in y, so at max y or min y
+        const float yx = sc >= 0.f ? fkey_inv(ymm[c]) : fkey_inv(ymm[ymm_ld + c]);
+        const float zm = relu_f(fmaf(yx, sc, sh));
+        atomicMax(reinterpret_cast<unsigned*>(amax_z), __float_as_uint(zm));
+    }
     if (rmean) {
         const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
         rmean[c] = (float)((double)momentum * mu + (1.0 - (double)momentum) * (double)rmean[c]);
@@ -318,12 +324,32 @@ __global__ void slab_sum_nc_kernel(const float* slab, int N, int nchunks, int R,
 }
 
 // out[c] (+)= sum_n in[n][c]
-__global__ void col_sum_kernel(const float* in, int N, int C, float* out, int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+// up to three independent column sums in one launch (blockIdx.y selects the pair); 64 columns per block, the rows
+// split over the 4 waves (8 loads in flight per lane), folded in a fixed order: deterministic
+struct ColSum3 { const float* in[3]; float* out[3]; };
+__global__ __launch_bounds__(256) void col_sum_kernel(ColSum3 cs, int N, int C, int accumulate) {
+    __shared__ double red[4][64];
+    const float* in = cs.in[blockIdx.y];
+    float* out = cs.out[blockIdx.y];
+    const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
     double s = 0.0;
-    for (int n = 0; n < N; ++n) s += in[(long long)n * C + c];
-    out[c] = accumulate ? out[c] + (float)s : (float)s;
+    if (c < C) {
+        int n = grp;
+        for (; n + 28 < N; n += 32) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = in[(long long)(n + 4 * k) * C + c];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += v[k];
+        }
+        for (; n < N; n += 4) s += in[(long long)n * C + c];
+    }
+    red[grp][cl] = s;
+    __syncthreads();
+    if (grp == 0 && c < C) {
+        const float r = (float)(red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
+        out[c] = accumulate ? out[c] + r : r;
+    }
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -353,7 +379,7 @@ __global__ __launch_bounds__(256) void norm_apply_fwd_kernel(const float* y, int
                 const float4 v = ld4(y + ((long long)(n * H + 2 * ho + (e >> 1)) * W + 2 * wo + (e & 1)) * ldy + c4);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    float z = f4get(v, j) * np.s[n * np.sn + c4 + j] + np.t[n * np.sn + c4 + j];
+                    float z = fmaf(f4get(v, j), np.s[n * np.sn + c4 + j], np.t[n * np.sn + c4 + j]);
                     if (RELU) z = relu_f(z);
                     if (z > o[j] || isnan(z)) o[j] = z;
                 }
@@ -363,7 +389,7 @@ __global__ __launch_bounds__(256) void norm_apply_fwd_kernel(const float* y, int
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int c = c4 + j;
-                float z = f4get(v, j) * np.s[n * np.sn + c] + np.t[n * np.sn + c];
+                float z = fmaf(f4get(v, j), np.s[n * np.sn + c], np.t[n * np.sn + c]);
                 if (RELU) z = relu_f(z);
                 if constexpr (FILM) z = fp.a[n * fp.an + c] * z + fp.b[n * fp.bn + c];
                 if constexpr (RESID) {
@@ -504,9 +530,21 @@ CDM_API int cdm_slab_colsum(const float* slab, int ntiles, int R, int C, double*
 
 CDM_API int cdm_bn_fwd_finalize(const double* part, int nparts, int R, int C, double count, const float* gamma,
                                 const float* beta, float* rmean, float* rvar, long long* nbt, float momentum, float eps,
-                                float* mean, float* invstd, float* scale, float* shift, void* stream) {
+                                float* mean, float* invstd, float* scale, float* shift, const int* ymm, int ymm_ld,
+                                float* amax_z, void* stream) {
+    if (ymm && !amax_z) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, S(stream), part, nparts, R, C, count,
-                       gamma, beta, rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift);
+                       gamma, beta, rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift, ymm, ymm_ld, amax_z);
+    return cdm_status();
+}
+__global__ void fill_i32_kernel(int* p, long long n, int v) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+CDM_API int cdm_fill_i32(int* p, long long n, int v, void* stream) {
+    if (n <= 0) return 0;
+    long long b = (n + 255) / 256;
+    hipLaunchKernelGGL(fill_i32_kernel, dim3((int)(b > 4096 ? 4096 : b)), dim3(256), 0, S(stream), p, n, v);
     return cdm_status();
 }
 
@@ -550,7 +588,15 @@ CDM_API int cdm_slab_sum_nc(const float* slab, int N, int nchunks, int R, int r,
 }
 
 CDM_API int cdm_col_sum(const float* in, int N, int C, float* out, int accumulate, void* stream) {
-    hipLaunchKernelGGL(col_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), in, N, C, out, accumulate);
+    ColSum3 cs{{in, nullptr, nullptr}, {out, nullptr, nullptr}};
+    hipLaunchKernelGGL(col_sum_kernel, dim3((C + 63) / 64, 1), dim3(256), 0, S(stream), cs, N, C, accumulate);
+    return cdm_status();
+}
+CDM_API int cdm_col_sum3(const float* in0, float* out0, const float* in1, float* out1, const float* in2, float* out2,
+                         int N, int C, void* stream) {
+    const int k = in2 ? 3 : (in1 ? 2 : 1);
+    ColSum3 cs{{in0, in1, in2}, {out0, out1, out2}};
+    hipLaunchKernelGGL(col_sum_kernel, dim3((C + 63) / 64, k), dim3(256), 0, S(stream), cs, N, C, 0);
     return cdm_status();
 }
 

@@ -118,6 +118,8 @@ class UNetEngine:
         # h3 train: BatchNorm backward fused into the staging of the layer's dgrad / wgrad (dy never written);
         # $CDM_FUSE_BN_BWD=0 keeps the separate apply kernel (A/B checks)
         self.fuse_bn_bwd = self.nterm == NT_H3 and os.environ.get("CDM_FUSE_BN_BWD", "1") != "0"
+        # h3 train: a dense BatchNorm + ReLU applied inside the next conv's staging ($CDM_FUSE_BN_FWD=0: apply kernel)
+        self.fuse_bn_fwd = self.nterm == NT_H3 and os.environ.get("CDM_FUSE_BN_FWD", "1") != "0"
         self.device = torch.device(device)
         self.layers = conv_layers(n_feat, height)
         self.L = {l.name: l for l in self.layers}
@@ -128,16 +130,56 @@ class UNetEngine:
         self._ones = torch.ones(4 * n_feat, device=self.device)
         self._zeros = torch.zeros(4 * n_feat, device=self.device)
         self._amax = torch.zeros(2, device=self.device)     # h3: max|A|, max|B| of the current launch
+        # h3 train: batched repack (3 launches per step); $CDM_BATCH_REPACK=0 keeps the per-layer launches (A/B)
+        self.batch_repack = os.environ.get("CDM_BATCH_REPACK", "1") != "0"
+        self._batch_key = None
 
     # ------------------------------------------------------------------------------------------
     # weight packing (OIHW / [Cin][Cout][kh][kw] -> GEMM layouts; eval: BatchNorm folded)
     # ------------------------------------------------------------------------------------------
+    def _repack_h3_train_batched(self, P, stream: int):
+        """h3 train mode: every 3x3 conv with C_in > 1 (and out.0) repacked in 3 launches — clear the max|W| slots,
+        max|W| per layer, the split images straight from OIHW (cdm_pack_split_conv3x3_batch)."""
+        nf = self.nf
+        specs = [(l.name, P[l.w], l.cin, l.cout, l.kc) for l in self.layers if l.cin > 1]
+        specs.append(("out.0", P["out.0.weight"], 2 * nf, nf, self.kc_out0))
+        key = tuple(w.data_ptr() for _, w, *_ in specs)
+        if self._batch_key != key:
+            import ctypes
+
+            class Job(ctypes.Structure):
+                _fields_ = [("W", ctypes.c_void_p), ("Cin", ctypes.c_int), ("Cout", ctypes.c_int), ("kc", ctypes.c_int),
+                            ("pad", ctypes.c_int), ("wpk_x", ctypes.c_void_p), ("wdg_x", ctypes.c_void_p),
+                            ("amax", ctypes.c_void_p)]
+            assert ctypes.sizeof(Job) == 48
+            slots = torch.zeros(len(specs), device=self.device)
+            arr = (Job * len(specs))()
+            for i, (name, W, cin, cout, kc) in enumerate(specs):
+                wx = self._buf(name + ".wpk_x", (_cdiv(9 * cin, 16) * 3 * cout * 16,), torch.bfloat16)
+                wdx = self._buf(name + ".wdg_x", (_cdiv(9 * cout, 16) * 3 * cin * 16,), torch.bfloat16)
+                self.pk[name + ".wpk_x"], self.pk[name + ".wdg_x"] = wx, wdx
+                self.pk[name + ".wpk_amax"] = self.pk[name + ".wdg_amax"] = slots[i:i + 1]
+                arr[i] = Job(W.data_ptr(), cin, cout, kc, 0, wx.data_ptr(), wdx.data_ptr(), slots.data_ptr() + 4 * i)
+            raw = bytes(memoryview(arr).cast("B"))
+            self._batch_jobs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+            self._batch_slots, self._batch_n = slots, len(specs)
+            self._batch_max = max(cin * cout * 9 for _, _, cin, cout, _ in specs)
+            self._batch_key = key
+        lb = lib()
+        lb.cdm_zero_f32(_p(self._batch_slots), self._batch_n, stream)
+        lb.cdm_pack_split_conv3x3_batch(_p(self._batch_jobs), self._batch_n, self._batch_max, stream)
+
     def repack(self, P: Dict[str, torch.Tensor], train: bool, stream: int, key=None):
         if key is not None and self._pk_key == (key, train):
             return
         lb = lib(); nf = self.nf
+        batched = train and self.nterm == NT_H3 and self.batch_repack
+        if batched:
+            self._repack_h3_train_batched(P, stream)
         for l in self.layers:
             W, b = P[l.w], P[l.b]
+            if batched and l.cin > 1:
+                continue
             if train:
                 wpk = self._buf(l.name + ".wpk", (9 * l.cin, l.cout))
                 wdg = (self._buf(l.name + ".wdg", (9 * l.cout, l.cin))) if l.cin > 1 else None
@@ -160,14 +202,15 @@ class UNetEngine:
                 if l.cin > 1:
                     self._split(l.name + ".wpk_e", 9 * l.cin, l.cout, stream)
         # out.0 (GroupNorm follows: never folded)
-        wpk = self._buf("out.0.wpk", (9 * 2 * nf, nf))
-        wdg = self._buf("out.0.wdg", (9 * nf, 2 * nf))
-        lb.cdm_pack_conv3x3(_p(P["out.0.weight"]), _p(P["out.0.bias"]), 2 * nf, nf, None, None, None, None, 0.0,
-                            _p(wpk), None, _p(wdg) if train else None, self.kc_out0, stream)
-        self.pk["out.0.wpk"], self.pk["out.0.wdg"] = wpk, wdg
-        self._split("out.0.wpk", 9 * 2 * nf, nf, stream)
-        if train:
-            self._split("out.0.wdg", 9 * nf, 2 * nf, stream)
+        if not batched:
+            wpk = self._buf("out.0.wpk", (9 * 2 * nf, nf))
+            wdg = self._buf("out.0.wdg", (9 * nf, 2 * nf))
+            lb.cdm_pack_conv3x3(_p(P["out.0.weight"]), _p(P["out.0.bias"]), 2 * nf, nf, None, None, None, None, 0.0,
+                                _p(wpk), None, _p(wdg) if train else None, self.kc_out0, stream)
+            self.pk["out.0.wpk"], self.pk["out.0.wdg"] = wpk, wdg
+            self._split("out.0.wpk", 9 * 2 * nf, nf, stream)
+            if train:
+                self._split("out.0.wdg", 9 * nf, 2 * nf, stream)
         for name, cin in (("up1.model.0", 4 * nf), ("up2.model.0", 2 * nf)):
             wt = self._buf(name + ".wt", (cin, 4 * nf))
             wtT = self._buf(name + ".wtT", (4 * nf, cin))
@@ -217,15 +260,25 @@ class UNetEngine:
         self.pk[name + "_x"] = xb
 
     def conv3x3(self, key, x_p, B, S, cin, ldx, bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, s,
-                amax_x=None, amax_y=None):
+                amax_x=None, amax_y=None, pre=None, ymm=None):
         """3x3 conv (fwd or dgrad) with the packed weights pk[key], in this engine's conv arithmetic.
 
         h3 only: amax_x = device max|x| written by x's producer (None: measured here by a separate pass);
-        amax_y = slot that receives max|y| for the next conv."""
+        amax_y = slot that receives max|y| for the next conv; pre = (scale, shift) pointers: the input is
+        relu(x * scale + shift) of the previous layer's pre-norm output, applied while staging; ymm = (ptr, ld):
+        per-channel max / min keys of y for the next layer's fused apply."""
         if self.nterm == NT_H3:
             if amax_x is None:
+                assert pre is None
                 amax_x = _p(self._amax)
                 lib().cdm_amax_f32(x_p, B * S * S, cin, ldx, amax_x, 0, s)
+            if pre is not None or ymm is not None:
+                ps, pt = pre if pre is not None else (None, None)
+                ym, yld = ymm if ymm is not None else (None, 0)
+                lib().cdm_conv3x3_fwd_h3_ex(x_p, B, S, S, cin, ldx, ps, pt, _p(self.pk[key + "_x"]), amax_x,
+                                            _p(self.pk[key + "_amax"]), bias_p, y_p, ldy, cout, flags, stats_p,
+                                            stats_ld, kc, amax_y, ym, yld, s)
+                return
             lib().cdm_conv3x3_fwd_h3(x_p, B, S, S, cin, ldx, _p(self.pk[key + "_x"]), amax_x,
                                      _p(self.pk[key + "_amax"]), bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc,
                                      amax_y, s)
@@ -235,6 +288,20 @@ class UNetEngine:
         else:
             lib().cdm_conv3x3_fwd(x_p, B, S, S, cin, ldx, _p(self.pk[key]), bias_p, y_p, ldy, cout, flags, stats_p,
                                   stats_ld, kc, s)
+
+    def fuses_bn_fwd(self, l: "LayerSpec", kind: str) -> bool:
+        """Producer l's train-mode BatchNorm apply (z = relu(y s + t)) runs inside the staging of the next conv (its
+        forward and its weight gradient): z is never written.  Needs the LDS-halo path for both convs (max / min
+        epilogue on l, BN-ReLU staging on the consumer) and the kernel-row weight gradient for the consumer."""
+        if not (self.fuse_bn_fwd and kind == "dense" and l.cin > 1):
+            return False
+        i = self.layers.index(l)
+        if i + 1 >= len(self.layers):
+            return False
+        c = self.layers[i + 1]
+        halo = lambda L: L.kc == 16 and L.S in (32, 64, 128, 256) and (L.S * L.S) % 256 == 0   # noqa: E731
+        return (halo(l) and halo(c) and c.cin == l.cout and c.cin <= 256 and c.cin % 128 == 0 and c.cout % 128 == 0
+                and c.S == l.S)
 
     def fuses_bn_bwd(self, l: "LayerSpec", kind: str) -> bool:
         """Layer l's BN backward runs inside its dgrad / wgrad staging (cdm_conv3x3_*_h3_bnbwd)."""
@@ -290,6 +357,10 @@ class UNetEngine:
         ws.sc_pending = (sc_w, sc_b, sc_split)
         if self.nterm == NT_H3:
             lb.cdm_zero_f32(_p(ws.amax), ws.amax.numel(), s)
+        if train and ws.fused_fwd:
+            half = ws.ymm.numel() // 2
+            lb.cdm_fill_i32(_p(ws.ymm), half, -2 ** 31, s)               # max keys
+            lb.cdm_fill_i32(_p(ws.ymm) + 4 * half, half, 2 ** 31 - 1, s)  # min keys
         # ---------------- encoder ----------------
         for l in self.layers[:10]:
             self._conv_bn_fwd(ws, P, l, s, x)
@@ -371,15 +442,23 @@ class UNetEngine:
                 ntiles = B * _cdiv(S * S, CHUNK)
             else:
                 yslot = self._slot(ws, "y:" + l.name) if l.name in ws.fused else None
+                src, pre = self._src_pre(ws, l)
+                ymm = ws.ymm_of(l) if l.name in ws.fused_fwd else None
                 self.conv3x3(l.name + ".wpk", src.p, B, S, l.cin, src.ld, _p(P[l.b]), _p(y), l.cout, l.cout, 0,
-                             _p(ws.slab), l.cout, l.kc, s, amax_x=self._src_slot(ws, l), amax_y=yslot)
+                             _p(ws.slab), l.cout, l.kc, s, amax_x=self._src_slot(ws, l), amax_y=yslot, pre=pre,
+                             ymm=ymm)
                 ntiles = _cdiv(npix, CHUNK)
             bn = l.bn
             nparts = fold(ws, _p(ws.slab), ntiles, 2, l.cout, s)
+            fused_fwd = l.name in ws.fused_fwd
+            ymm_p, ymm_ld = ws.ymm_of(l) if fused_fwd else (None, 0)
             lb.cdm_bn_fwd_finalize(_p(ws.dpart), nparts, 2, l.cout, float(npix), _p(P[bn + ".weight"]),
                                    _p(P[bn + ".bias"]), _p(P[bn + ".running_mean"]), _p(P[bn + ".running_var"]),
                                    _p(P[bn + ".num_batches_tracked"]), BN_MOM, BN_EPS, _p(st["mean"]),
-                                   _p(st["invstd"]), _p(st["scale"]), _p(st["shift"]), s)
+                                   _p(st["invstd"]), _p(st["scale"]), _p(st["shift"]), ymm_p, ymm_ld,
+                                   self._dst_slot(ws, l) if fused_fwd else None, s)
+            if fused_fwd:
+                return                    # z = relu(y s + t) is applied by the next conv's staging
             scale, shift, relu = st["scale"], st["shift"], APPLY_RELU
         else:
             kind = ws.dst_kind[l.name]
@@ -448,9 +527,9 @@ class UNetEngine:
         H1, H2 = H // 2, H // 4
         P0, P1, P2 = B * H * H, B * H1 * H1, B * H2 * H2
         # ---------------- out.3 (nf -> 1) ----------------
-        nch = _cdiv(H * H, CHUNK)
-        lb.cdm_conv3x3_cout1_wgrad(_p(deps), _p(ws.zO), nf, B, H, H, nf, CHUNK, _p(ws.slab), s)
-        S = fold(ws, _p(ws.slab), B * nch, 9, nf, s)
+        R = cout1_band_rows(B, H)
+        lb.cdm_conv3x3_cout1_wgrad(_p(deps), _p(ws.zO), nf, B, H, H, nf, -R, _p(ws.slab), s)
+        S = fold(ws, _p(ws.slab), B * H // R, 9, nf, s)
         lb.cdm_slab_sum_all(_p(ws.dpart), S, 9, 0, 9, nf, _p(G["out.3.weight"]), 1, 9, 0, s)
         if not out3_bias_done:
             _sum_into(deps, G["out.3.bias"], ws, s)
@@ -553,10 +632,14 @@ class UNetEngine:
                                      self._slot(ws, "g:" + l.name), self._slot(ws, "y:" + l.name), dslot, s)
             coef = (_p(st["scale"]), _p(st["shift"]), _p(st["mean"]), _p(st["invstd"]), _p(co[0]), _p(co[1]),
                     _p(co[2]))
-            src = ws.src[l.name]
+            src, pre = self._src_pre(ws, l)
             sp = wgrad_splits(B * S * S, C, 9 * l.cin)
-            lb.cdm_conv3x3_wgrad_h3_bnbwd(g.p, g.ld, _p(y), C, *coef, C, src.p, B, S, S, l.cin, src.ld, dslot,
-                                          self._src_slot(ws, l), sp, _p(ws.slab), s)
+            if pre is None:
+                lb.cdm_conv3x3_wgrad_h3_bnbwd(g.p, g.ld, _p(y), C, *coef, C, src.p, B, S, S, l.cin, src.ld, dslot,
+                                              self._src_slot(ws, l), sp, _p(ws.slab), s)
+            else:
+                lb.cdm_conv3x3_wgrad_h3_ex(g.p, g.ld, _p(y), C, *coef, C, src.p, B, S, S, l.cin, src.ld, pre[0],
+                                           pre[1], dslot, self._src_slot(ws, l), sp, _p(ws.slab), s)
             lb.cdm_slab_reduce(_p(ws.slab), sp, C, 9 * l.cin, _p(G[l.w]), 9 * l.cin, 1, 9, l.cin, 0, 1.0, s)
             dgd = ws.dgrad_dst[l.name]
             key = l.name + ".wdg"
@@ -569,16 +652,26 @@ class UNetEngine:
         lb.cdm_norm_apply_bwd(mode, g.p, g.ld, _p(y), C, B, S, S, C, _p(st["scale"]), _p(st["shift"]), 0,
                               _p(st["mean"]), _p(st["invstd"]), 0, 1, _p(film_a), film_an, _p(co[0]), _p(co[1]),
                               _p(co[2]), 0, dy.p, dy.ld, dslot, s)
-        src = ws.src[l.name]
+        src, pre = self._src_pre(ws, l)
         if l.cin == 1:
             lb.cdm_conv3x3_cin1_wgrad(dy.p, dy.ld, _p(ws.x_in), B, S, S, C, CHUNK, _p(ws.slab), s)
             nparts = fold(ws, _p(ws.slab), B * _cdiv(S * S, CHUNK), 10, C, s)
             lb.cdm_slab_sum_all(_p(ws.dpart), nparts, 10, 0, 9, C, _p(G[l.w]), 1, 9, 0, s)
             return
-        self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s, amax_dy=dslot, amax_x=self._src_slot(ws, l))
+        self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s, amax_dy=dslot, amax_x=self._src_slot(ws, l), pre=pre)
         dgd = ws.dgrad_dst[l.name]
         self.conv3x3(l.name + ".wdg", dy.p, B, S, C, dy.ld, None, dgd.p, dgd.ld, l.cin,
                      EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s, amax_x=dslot, amax_y=gslot)
+
+    def _src_pre(self, ws, l: "LayerSpec"):
+        """(input activation, BN-ReLU transform or None) of conv l in train mode: a fused producer hands over its
+        pre-norm output y and its (scale, shift) instead of z."""
+        i = self.layers.index(l)
+        if i > 0 and self.layers[i - 1].name in ws.fused_fwd:
+            p = self.layers[i - 1]
+            st = ws.bn[p.name]
+            return Act(ws.y[p.name], p.cout), (_p(st["scale"]), _p(st["shift"]))
+        return ws.src[l.name], None
 
     def _dgrad_amax_slot(self, ws, l: "LayerSpec"):
         """Slot that receives max|dgrad output| of layer l: the grad wrt a ConvT output (h3 ConvT backward) or
@@ -591,9 +684,14 @@ class UNetEngine:
     # the dgrads that write the gradient wrt a ConvT output (gT1 / gT2) also record its max for the h3 ConvT bwd
     _CONVT_GRAD_PRODUCERS = {"up1.model.1.conv1": "up1.model.0", "up2.model.1.conv1": "up2.model.0"}
 
-    def _wgrad3x3(self, ws, dy: Act, x: Act, B, S, cin, cout, gW, s, amax_dy=None, amax_x=None):
+    def _wgrad3x3(self, ws, dy: Act, x: Act, B, S, cin, cout, gW, s, amax_dy=None, amax_x=None, pre=None):
         lb = lib()
         sp = wgrad_splits(B * S * S, cout, 9 * cin)
+        if pre is not None:        # X = relu(x s + t) of a fused producer (h3, kernel-row weight gradient)
+            lb.cdm_conv3x3_wgrad_h3_ex(dy.p, dy.ld, None, 0, None, None, None, None, None, None, None, cout, x.p, B, S,
+                                       S, cin, x.ld, pre[0], pre[1], amax_dy, amax_x, sp, _p(ws.slab), s)
+            lb.cdm_slab_reduce(_p(ws.slab), sp, cout, 9 * cin, _p(gW), 9 * cin, 1, 9, cin, 0, 1.0, s)
+            return
         if self.nterm == NT_H3:
             am = _p(self._amax)
             if amax_dy is None:
@@ -648,10 +746,9 @@ class UNetEngine:
         co = ws.gcoef
         lb.cdm_gn_bwd_finalize(_p(ws.slab), B, nch, C, GN_GROUPS, float(S * S * cpg), S * S, _p(P[name + ".weight"]),
                                _p(st["invstd"]), _p(co[0]), _p(co[1]), _p(co[2]), _p(co[3]), _p(co[4]), _p(co[5]), s)
-        lb.cdm_col_sum(_p(co[3]), B, C, _p(G[name + ".weight"]), 0, s)
-        lb.cdm_col_sum(_p(co[4]), B, C, _p(G[name + ".bias"]), 0, s)
-        if bias_name is not None:
-            lb.cdm_col_sum(_p(co[5]), B, C, _p(G[bias_name]), 0, s)
+        lb.cdm_col_sum3(_p(co[3]), _p(G[name + ".weight"]), _p(co[4]), _p(G[name + ".bias"]),
+                        _p(co[5]) if bias_name is not None else None,
+                        _p(G[bias_name]) if bias_name is not None else None, B, C, s)
         lb.cdm_norm_apply_bwd(mode, g.p, g.ld, y.p, y.ld, B, S, S, C, _p(st["scale"]), _p(st["shift"]), C,
                               _p(st["mean"]), _p(st["invstd"]), GN_GROUPS, cpg, _p(film_a), film_an, _p(co[0]),
                               _p(co[1]), _p(co[2]), C, dy.p, dy.ld, amax, s)
@@ -676,6 +773,15 @@ def fold(ws, slab_ptr: int, ntiles: int, R: int, C: int, stream: int) -> int:
     S = max(1, min(ntiles, max(1, 512 // _cdiv(C, 64)), ws.dpart.numel() // max(1, R * C)))
     lib().cdm_slab_colsum(slab_ptr, ntiles, R, C, _p(ws.dpart), S, stream)
     return S
+
+
+def cout1_band_rows(B: int, H: int) -> int:
+    """Rows per block of the out.3 weight-gradient band kernel: the largest divisor of H that still gives >= 1024
+    blocks (B=256 at 64x64: 16 rows -> 1024 blocks)."""
+    R = H
+    while R > 1 and (B * H // R < 1024 or H % R):
+        R -= 1
+    return R
 
 
 def wgrad_splits(K: int, M: int, N: int) -> int:
@@ -722,6 +828,7 @@ class Workspace:
         # per conv-BN layer: y (pre-norm), z destinations, BN coefficients
         L = eng.layers
         self.y, self.src, self.dst, self.dst_kind, self.bn = {}, {}, {}, {}, {}
+        self._no_z = torch.empty(0, device=dev)
         z = {}
         for l in L:
             npx = B * l.S * l.S
@@ -738,10 +845,12 @@ class Workspace:
         kinds["up1.model.2.conv2"] = "film"
         kinds["up2.model.2.conv2"] = "plain"
         self.dst_kind = kinds
+        self.fused_fwd = {l.name for l in L if train and eng.fuses_bn_fwd(l, kinds[l.name])}
         for l in L:
             k = kinds[l.name]
             if k == "dense":
-                z[l.name] = Act(E(B * l.S * l.S, l.cout), l.cout)
+                # a fused producer's z is never materialised (the consumer stages relu(y s + t) itself)
+                z[l.name] = Act(E(B * l.S * l.S, l.cout) if l.name not in self.fused_fwd else self._no_z, l.cout)
                 self.dst[l.name] = z[l.name]
         self.dst["init_conv.conv2"] = self.catO.sl(nf, nf)
         self.dst["down1.model.1.conv2"] = self.catU2.sl(nf, nf)
@@ -764,6 +873,10 @@ class Workspace:
             else:
                 self.src[l.name] = self.dst[prev[l.name]]
         self.slab = E(self._slab_floats())
+        # per fused layer: max / min keys of its pre-norm output ([2][n_fused][Cmax] int32, refilled every forward)
+        self._ymm_idx = {n: i for i, n in enumerate(sorted(self.fused_fwd))}
+        self._ymm_C = max([l.cout for l in L] + [1])
+        self.ymm = torch.empty(2 * max(1, len(self.fused_fwd)) * self._ymm_C, dtype=torch.int32, device=dev)
         self.amax = torch.zeros(192, device=dev)  # h3 operand maxima, one slot per producer (UNetEngine._slot)
         self.aslot = {}
         self.dpart = torch.empty(10 * 32768 + 4096, device=dev, dtype=torch.float64)
@@ -811,6 +924,11 @@ class Workspace:
         else:
             self.fused, self.g_amax_key = set(), {}
 
+    def ymm_of(self, l) -> tuple:
+        """(pointer, ld) of fused layer l's max keys; its min keys sit ld ints further."""
+        half = self.ymm.numel() // 2
+        return self.ymm.data_ptr() + 4 * self._ymm_idx[l.name] * self._ymm_C, half
+
     def _wire_fused_bn_bwd(self, eng, L, kinds):
         """Fused layers read g and write their dgrad without a dy buffer in between, so g and the dgrad output
         must differ: walking the backward order, each fused layer writes its dgrad into the other buffer of its
@@ -848,6 +966,7 @@ class Workspace:
         nf, H = eng.nf, eng.H
         P0 = B * H * H
         need = _cdiv(P0, CHUNK) * 10 * 2 * nf          # stats / bwd partials at full res (R <= 10)
+        need = max(need, B * H // cout1_band_rows(B, H) * 9 * nf)   # out.3 weight-gradient band partials
         if self.train:
             for l in eng.layers:                         # conv wgrad split-K slabs
                 if l.cin > 1:

@@ -53,6 +53,15 @@ int cdm_split_bf16x3(const float* b, long long ldb, int K, int N, void* out, voi
 int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
                        const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags, float* stats,
                        int stats_ld, int kc, float* amax_y, void* stream);
+/* cdm_conv3x3_fwd_h3 with the train-mode Conv -> BatchNorm -> ReLU fusions (LDS-halo shapes only):
+ * pre_s / pre_t (optional): the input is relu(x * pre_s[c] + pre_t[c]) computed while staging (x = the previous
+ * layer's pre-norm output; its BatchNorm apply is never materialised; *amax_x must be max of that input);
+ * ymm (optional, needs stats): per output channel max / min of y as ordered-int keys ymm[c] / ymm[ymm_ld + c],
+ * cleared by the caller to INT_MIN / INT_MAX (cdm_fill_i32); cdm_bn_fwd_finalize turns them into max|z| */
+int cdm_conv3x3_fwd_h3_ex(const float* x, int N, int H, int W, int Cin, int ldx, const float* pre_s, const float* pre_t,
+                          const void* wx, const float* amax_x, const float* amax_w, const float* bias, float* y, int ldy,
+                          int Cout, int flags, float* stats, int stats_ld, int kc, float* amax_y, int* ymm, int ymm_ld,
+                          void* stream);
 /* timing ablations of the h3 LDS-halo conv (64x64 maps, no bias / stats; tools/conv_ablation.py): abl bits
  * 1 fragment prefetch, 2 MFMAs doubled, 4 B staged once, 8 halo without the term split (results meaningless);
  * bits 16+: tiles per block (0 -> 1) */
@@ -80,8 +89,21 @@ int cdm_conv3x3_wgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy,
                                const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
                                int Cout, const float* x, int N, int H, int W, int Cin, int ldx, const float* amax_dy,
                                const float* amax_x, int splits, float* slab, void* stream);
+/* the kernel-row weight gradient with both staging fusions selectable: y (+ s, t, mean, invstd, A, B, Cc) non-null:
+ * dY = the BatchNorm backward of g (as cdm_conv3x3_wgrad_h3_bnbwd), else dY = g; x_s / x_t non-null: the X operand
+ * is relu(x * x_s[c] + x_t[c]).  Cin % 128 == Cout % 128 == 0, W % 16 == 0. */
+int cdm_conv3x3_wgrad_h3_ex(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
+                            const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
+                            int Cout, const float* x, int N, int H, int W, int Cin, int ldx, const float* x_s,
+                            const float* x_t, const float* amax_dy, const float* amax_x, int splits, float* slab,
+                            void* stream);
 /* fp32 [K][N] (ld ldb) -> [ceil(K/16)][3][N][16]: planes 0/1 = fp16 hi/lo of b * 2^(14-e), max|b| = *amax < 2^e */
 int cdm_split_f16x2(const float* b, long long ldb, int K, int N, const float* amax, void* out, void* stream);
+/* batched train-mode repack: jobs_dev = device array of njobs records
+ *   { const float* W (OIHW); int Cin, Cout, kc, pad; bf16* wpk_x; bf16* wdg_x (may be null); float* amax; }
+ * (64-bit pointers, 48 bytes per record); writes max|W| (atomic max into a cleared *amax) and the two h3 split
+ * images of cdm_pack_conv3x3 + cdm_split_f16x2 directly from W.  max_w_elems = the largest Cout * Cin * 9. */
+int cdm_pack_split_conv3x3_batch(const void* jobs_dev, int njobs, long long max_w_elems, void* stream);
 /* *out = max(accumulate ? *out : 0, max |x[r*ld + c]|), r < rows, c < C (atomic max, graph-capturable) */
 int cdm_amax_f32(const float* x, long long rows, int C, long long ld, float* out, int accumulate, void* stream);
 /* ---- sample statistics (csrc/stats.hip) --------------------------------------------------------
@@ -153,7 +175,12 @@ int cdm_slab_colsum(const float* slab, int ntiles, int R, int C, double* part, i
 /* BatchNorm2d train statistics + running-stat update (diffusion_utilities.py:28,35; momentum 0.1, eps 1e-5) */
 int cdm_bn_fwd_finalize(const double* part, int nparts, int R, int C, double count, const float* gamma,
                         const float* beta, float* rmean, float* rvar, long long* nbt, float momentum, float eps,
-                        float* mean, float* invstd, float* scale, float* shift, void* stream);
+                        float* mean, float* invstd, float* scale, float* shift, const int* ymm, int ymm_ld,
+                        float* amax_z, void* stream);
+/* (ymm optional: the per-channel max / min keys of the layer's y from cdm_conv3x3_fwd_h3_ex; amax_z then receives
+ *  the exact max over the layer of relu(fmaf(y, scale, shift)) by an atomic max, for the consumer's h3 scale) */
+/* p[0..n) = v */
+int cdm_fill_i32(int* p, long long n, int v, void* stream);
 /* BatchNorm2d eval (running statistics) */
 int cdm_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
                        float* mean, float* invstd, float* scale, float* shift, void* stream);
@@ -168,6 +195,9 @@ int cdm_gn_bwd_finalize(const float* slab, int N, int nchunks, int C, int G, dou
                         float* pdbias, void* stream);
 int cdm_slab_sum_nc(const float* slab, int N, int nchunks, int R, int r, int C, float* out, void* stream);
 int cdm_col_sum(const float* in, int N, int C, float* out, int accumulate, void* stream);
+/* up to three column sums out_k[c] = sum_n in_k[n][c] in one launch (in1 / in2 may be null) */
+int cdm_col_sum3(const float* in0, float* out0, const float* in1, float* out1, const float* in2, float* out2, int N,
+                 int C, void* stream);
 /* out = [MaxPool2d(2)]([cemb*](ReLU(y*s+t))[+temb])[+ 1x1 shortcut(x)]  — flags 1 pool, 2 FiLM, 4 resid, 8 relu
  * (BN/GN apply diffusion_utilities.py:28-29; MaxPool2d :109; random shortcut :54-55; FiLM ContextUnet.py:57-58) */
 int cdm_norm_apply_fwd(int flags, const float* y, int ldy, int N, int H, int W, int C, const float* s, const float* t,
@@ -195,6 +225,8 @@ int cdm_conv3x3_cout1_fwd(const float* z, int ldz, int N, int H, int W, int C, c
                           float* out, void* stream);
 int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int C, const float* w, float* dz, int lddz,
                             void* stream);
+/* weight gradient partials: csize > 0: per (image, csize-pixel chunk) [N][chunks][9][C]; csize = -R (band form, H % R
+ * == 0): one block per R whole rows, every z pixel read once, partials [N * H / R][9][C] */
 int cdm_conv3x3_cout1_wgrad(const float* deps, const float* z, int ldz, int N, int H, int W, int C, int csize,
                             float* slab, void* stream);
 /* to_vec: AvgPool2d(h/4) + GELU (ContextUnet.py:17) */

@@ -48,6 +48,7 @@ def _dry_run(monkeypatch, nf, B, math, H=64, train=True):
     rec = _Recorder(protos)
     monkeypatch.setattr(E, "lib", lambda: rec)
     eng = E.UNetEngine(nf, 6, H, "cpu", math)
+    _dry_run.last_eng = eng
     from cdm_amd.model import ContextUnet
     torch.manual_seed(0)
     m = ContextUnet(1, nf, 6, H, conv_math=math)
@@ -74,7 +75,8 @@ def _dry_run(monkeypatch, nf, B, math, H=64, train=True):
         elif isinstance(o, (list, tuple)):
             for v in o:
                 reg(v)
-    for o in (P, G, eng.pk, vars(ws), [x, t, c, sc_w, sc_b, deps, eng._amax, eng._ones, eng._zeros]):
+    for o in (P, G, eng.pk, vars(ws), [x, t, c, sc_w, sc_b, deps, eng._amax, eng._ones, eng._zeros],
+              [getattr(eng, "_batch_jobs", None), getattr(eng, "_batch_slots", None)]):
         reg(o)
     return rec.calls, protos, live
 
@@ -124,8 +126,47 @@ def test_launch_arguments_stay_in_bounds(monkeypatch, nf, B, math, H, train):
             need(name, a, a["slab"], _eff_splits(a["K"], a["splits"]) * a["M"] * a["N"] * 4, "slab")
         elif name == "cdm_gemm_f32" and _eff_splits(a["K"], a["splits"]) > 1:
             need(name, a, a["slab"], _eff_splits(a["K"], a["splits"]) * a["M"] * a["N"] * 4, "slab")
+        elif name == "cdm_conv3x3_cout1_wgrad":
+            nblk = a["N"] * a["H"] // -a["csize"] if a["csize"] < 0 else a["N"] * -(-a["H"] * a["W"] // a["csize"])
+            need(name, a, a["slab"], nblk * 9 * a["C"] * 4, "slab")
         elif name == "cdm_slab_reduce":
             need(name, a, a["slab"], a["splits"] * a["M"] * a["N"] * 4, "slab")
+        if name == "cdm_pack_split_conv3x3_batch":
+            import numpy as np
+            tab = _dry_run.last_eng._batch_jobs.numpy()
+            assert a["jobs_dev"] == _dry_run.last_eng._batch_jobs.data_ptr() and a["njobs"] * 48 == tab.size
+            for j in range(a["njobs"]):
+                rec = tab[48 * j:48 * (j + 1)]
+                Wp, wx, wd, am = (int(np.frombuffer(rec[o:o + 8].tobytes(), np.uint64)[0]) for o in (0, 24, 32, 40))
+                cin, cout, kc = (int(np.frombuffer(rec[o:o + 4].tobytes(), np.int32)[0]) for o in (8, 12, 16))
+                assert cin * cout * 9 <= a["max_w_elems"]
+                need(name, a, Wp, cin * cout * 9 * 4, f"job {j} W")
+                need(name, a, wx, -(-9 * cin // 16) * 3 * cout * 16 * 2, f"job {j} wpk_x")
+                if wd:
+                    need(name, a, wd, -(-9 * cout // 16) * 3 * cin * 16 * 2, f"job {j} wdg_x")
+                need(name, a, am, 4, f"job {j} amax")
+        if name == "cdm_conv3x3_fwd_h3_ex":
+            Pn = a["N"] * a["H"] * a["W"]
+            need(name, a, a["x"], ((Pn - 1) * a["ldx"] + a["Cin"]) * 4, "x")
+            need(name, a, a["y"], ((Pn - 1) * a["ldy"] + a["Cout"]) * 4, "y")
+            if a["pre_s"]:
+                need(name, a, a["pre_s"], a["Cin"] * 4, "pre_s"); need(name, a, a["pre_t"], a["Cin"] * 4, "pre_t")
+            if a["ymm"]:
+                need(name, a, a["ymm"], a["Cout"] * 4, "ymm max")
+                need(name, a, a["ymm"] + 4 * a["ymm_ld"], a["Cout"] * 4, "ymm min")
+        if name == "cdm_conv3x3_wgrad_h3_ex":
+            Pn = a["N"] * a["H"] * a["W"]
+            need(name, a, a["g"], ((Pn - 1) * a["ldg"] + a["Cout"]) * 4, "g")
+            if a["y"]:
+                need(name, a, a["y"], ((Pn - 1) * a["ldy"] + a["Cout"]) * 4, "y")
+            need(name, a, a["x"], ((Pn - 1) * a["ldx"] + a["Cin"]) * 4, "x")
+            if a["x_s"]:
+                need(name, a, a["x_s"], a["Cin"] * 4, "x_s"); need(name, a, a["x_t"], a["Cin"] * 4, "x_t")
+            K = a["N"] * a["H"] * a["W"]
+            need(name, a, a["slab"], _eff_splits(K, a["splits"]) * a["Cout"] * 9 * a["Cin"] * 4, "slab")
+        if name == "cdm_bn_fwd_finalize" and a["ymm"]:
+            need(name, a, a["ymm"], a["C"] * 4, "ymm max")
+            need(name, a, a["ymm"] + 4 * a["ymm_ld"], a["C"] * 4, "ymm min")
         if name == "cdm_conv3x3_dgrad_h3_bnbwd":
             Pn = a["N"] * a["H"] * a["W"]
             need(name, a, a["g"], ((Pn - 1) * a["ldg"] + a["C"]) * 4, "g")

@@ -486,3 +486,35 @@ def test_conv3x3_h3_bench_launch_shape(L):
                 xs = xp[:, ky:ky + H, kx:kx + H, :].reshape(P, C)
                 wref[:, :, ky, kx] = gyd.t() @ xs
         _close(dW, wref.float(), 5e-5)
+
+
+@pytest.mark.parametrize("nf", [8, 128])
+def test_batched_repack_equals_per_layer(L, nf):
+    """h3 train repack in 3 launches (cdm_pack_split_conv3x3_batch) == the per-layer pack + amax + split path, bit for
+    bit: every split image (term planes 0 and 1; h3 leaves the x6 lo plane unused) and every max|W| (nf=8 covers the
+    tap-major kc=0 K order, nf=128 the chunk-major one)."""
+    import cdm_amd.engine as E
+    from cdm_amd import ContextUnet
+    torch.manual_seed(3)
+    m = ContextUnet(1, nf, 6, 64, conv_math="h3").cuda()
+    P = {k: v.detach() for k, v in list(m.named_parameters()) + list(m.named_buffers())}
+    out = []
+    for batched in (True, False):
+        eng = E.UNetEngine(nf, 6, 64, "cuda", "h3")
+        eng.batch_repack = batched
+        eng.repack(P, True, _s())
+        torch.cuda.synchronize()
+        out.append({k: v.clone() for k, v in eng.pk.items() if k.endswith(("_x", "_amax"))})
+    a, b = out
+    shapes = {l.name: (l.cin, l.cout) for l in E.conv_layers(nf, 64) if l.cin > 1}
+    shapes["out.0"] = (2 * nf, nf)
+    n = 0
+    for name, (cin, cout) in shapes.items():
+        for kind, N in ((".wpk", cout), (".wdg", cin)):
+            k = name + kind
+            assert torch.equal(a[k + "_amax"], b[k + "_amax"]), k
+            ta = a[k + "_x"].view(torch.int16).view(-1, 3, N * 16)[:, :2]
+            tb = b[k + "_x"].view(torch.int16).view(-1, 3, N * 16)[:, :2]
+            assert torch.equal(ta, tb), k
+            n += 1
+    assert n == 2 * len(shapes)

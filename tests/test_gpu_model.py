@@ -252,3 +252,39 @@ def test_eval_forward_under_grad_mode():
     assert torch.equal(out.detach(), ref)
     with pytest.raises(NotImplementedError):
         out.sum().backward()
+
+
+@pytest.mark.parametrize("B", [2, 5])
+def test_fused_bn_fwd_bit_exact_nf128(B):
+    """h3 train at n_feat=128: the 12 dense BatchNorm + ReLU applies fused into the next conv's staging (forward and
+    weight gradient; z never written; its h3 scale from the producer's per-channel max / min) == the separate apply
+    kernel ($CDM_FUSE_BN_FWD=0), bit for bit: output, every gradient, BatchNorm running statistics."""
+    nf, T = 128, 1500
+    g = torch.Generator().manual_seed(15)
+    x = torch.rand(B, 1, 64, 64, generator=g); noise = torch.randn(B, 1, 64, 64, generator=g)
+    c = torch.rand(B, 6, generator=g); tt = torch.randint(1, T + 1, (B,), generator=g)
+    _, _, ab = R.make_schedule(T)
+    xp = R.perturb_input(x, tt, noise, ab)
+    import cdm_amd.model as M
+    eng = M.get_engine(nf, 6, 64, torch.device("cuda", torch.cuda.current_device()), "h3")
+    res = []
+    try:
+        for fuse in (True, False):
+            eng.fuse_bn_fwd = fuse
+            M._WS.clear()
+            m = _model(nf, seed=16, math="h3").train()
+            torch.manual_seed(35)
+            pred = m(xp.cuda(), (tt / T).cuda(), c.cuda())
+            F.mse_loss(pred, noise.cuda()).backward()
+            ws = eng.workspace(B, True)
+            assert len(ws.fused_fwd) == (12 if fuse else 0)
+            res.append((pred.detach().cpu(), {k: p.grad.detach().cpu() for k, p in m.named_parameters()},
+                        {k: v.detach().cpu() for k, v in m.state_dict().items() if "running" in k}))
+    finally:
+        eng.fuse_bn_fwd = True
+        M._WS.clear()
+    assert torch.equal(res[0][0], res[1][0])
+    for k in res[1][1]:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k
+    for k in res[1][2]:
+        assert torch.equal(res[0][2][k], res[1][2][k]), k
