@@ -480,6 +480,10 @@ static int effective_splits(int K, int splits, int BK = 16) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+// 16-byte staging registers: a native vector, not HIP's uint4 struct — a struct copy lowers to a memcpy that SROA
+// leaves in an alloca, which AMDGPUPromoteAlloca then moves into LDS (every staged piece took a global -> LDS slot ->
+// register -> LDS round trip with a vmcnt(0) wait next to its load)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int NT_H3 = 4;
 
 // the power-of-two operand scale of NT_H3 (1 for the bf16 arithmetics or a missing / degenerate max)
@@ -597,7 +601,7 @@ struct StagePre {
     const float* amax;                   // NT_H3: max|W| the terms were split with (cdm_split_f16x2)
     float sc;
     int rr, kh; bool ok;
-    uint4 r[NS];
+    u32x4 r[NS];
     __device__ __forceinline__ float sc_of() const { return op_scale<NT>(amax); }
     __device__ __forceinline__ void init(int tid, int r0) {
         sc = op_scale<NT>(amax);
@@ -605,18 +609,18 @@ struct StagePre {
     }
     __device__ __forceinline__ void zero() {
 #pragma unroll
-        for (int t = 0; t < NS; ++t) r[t] = make_uint4(0, 0, 0, 0);
+        for (int t = 0; t < NS; ++t) r[t] = u32x4{0, 0, 0, 0};
     }
     __device__ __forceinline__ void gload(int, int kt) {
 #pragma unroll
         for (int t = 0; t < NS; ++t)
-            r[t] = ok ? *reinterpret_cast<const uint4*>(p + (((long long)kt * 3 + t) * rows + rr) * XBK + kh)
-                      : make_uint4(0, 0, 0, 0);
+            r[t] = ok ? *reinterpret_cast<const u32x4*>(p + (((long long)kt * 3 + t) * rows + rr) * XBK + kh)
+                      : u32x4{0, 0, 0, 0};
     }
     __device__ __forceinline__ void sstore(int tid, __bf16* base) const {
         __bf16* d = base + xoff(tid >> 1, (tid & 1) * 8);
 #pragma unroll
-        for (int t = 0; t < NS; ++t) *reinterpret_cast<uint4*>(d + t * XPLANE) = r[t];
+        for (int t = 0; t < NS; ++t) *reinterpret_cast<u32x4*>(d + t * XPLANE) = r[t];
     }
 };
 
@@ -827,7 +831,9 @@ constexpr int HTHREADS = 512;
 // tap's fragments are read during the current tap's MFMAs: 0.94 -> 0.84 ms), 2 every MFMA issued twice, 4 B
 // staged once (stale afterwards), 8 halo stored without the term split, 16 no barriers in the main loop,
 // 32 halo loaded for the first chunk only, 64 / 128 prefetch schedules: 2 reads per MFMA gap / all reads after the
-// tap's first MFMA
+// tap's first MFMA, 256 staggered halo split (waves 0-3 split + store the next chunk's halo after their last kernel
+// row's MFMAs, waves 4-7 before them, so each SIMD pairs one wave's VALU with its partner's MFMAs), 512 static
+// priority 1 for waves 4-7
 template <int NT, int WT, class EP, bool XCD_REMAP, int ABL = (NT >= 6 ? 0 : 1), class PRE = PreNone>
 __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const float* __restrict__ x, int H, int Cin,
                                                                       int ldx, const __bf16* __restrict__ wx3,
@@ -846,6 +852,9 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
+    if constexpr (ABL & 512) {
+        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    }
     // the block's tpb 256-pixel tiles, run one after the other: the next tile's first halo and B are fetched
     // during the current tile's last chunk, so only a block's first tile waits on HBM latency before its MFMAs.
     // XCD-aware: XCD x owns a contiguous tile range and its cnt blocks step through it together (tile
@@ -878,8 +887,13 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     f32x16 acc[2][2];
 
     // ---- halo staging: piece q = (halo pixel q>>2, channels 4(q&3)..+3); addresses fixed per block ----
+    // Every global load of the main loop is issued unconditionally (pieces outside the image load a valid dummy
+    // address and are zeroed where they are stored): with loads under branches the compiler can no longer count
+    // them and waits for vmcnt(0) — the B stores of a kernel row then waited on the next chunk's halo (HBM latency)
+    // and the halo split on the B loads just issued.
     float4 hreg[HQ];
-    const float* hsrc[HQ];          // chunk-0 source of piece j (nullptr: zero padding / past the halo)
+    const float* hsrc[HQ];          // chunk-0 source of piece j (a dummy in-bounds address when !hin[j])
+    bool hin[HQ];                   // piece j is inside the image (else zero padding / past the halo)
     int hdst[HQ];                   // its LDS offset within a term plane
     float4 yreg[PRE::on ? HQ : 1];  // PreBnBwd: the pre-norm activations of piece j
     const float* hysrc[PRE::on ? HQ : 1];
@@ -892,9 +906,10 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
             const int hr = hp / HC, hc = hp - hr * HC;
             const int ih = h0 - 1 + hr, iw = hc - 1;
             const bool in = q < HPX * 4 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)WT;
-            hsrc[j] = in ? x + ((long long)(img * H + ih) * WT + iw) * ldx + c4 * 4 : nullptr;
-            if constexpr (PRE::on)
-                hysrc[j] = in ? pre.y + ((long long)(img * H + ih) * WT + iw) * pre.ldy + c4 * 4 : nullptr;
+            const long long pix = in ? (long long)(img * H + ih) * WT + iw : 0;
+            hin[j] = in;
+            hsrc[j] = x + pix * ldx + c4 * 4;
+            if constexpr (PRE::on) hysrc[j] = pre.y + pix * pre.ldy + c4 * 4;
         }
     };
 #pragma unroll
@@ -909,8 +924,8 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         }
 #pragma unroll
         for (int j = 0; j < HQ; ++j) {
-            hreg[j] = hsrc[j] ? ld4(hsrc[j] + cc * 16) : f4zero();
-            if constexpr (PRE::on) yreg[j] = hysrc[j] ? ld4(hysrc[j] + cc * 16) : f4zero();
+            hreg[j] = ld4(hsrc[j] + cc * 16);
+            if constexpr (PRE::on) yreg[j] = ld4(hysrc[j] + cc * 16);
         }
     };
     auto store_halo = [&](__bf16* base, int cc) {
@@ -928,18 +943,16 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
             if (hdst[j] >= 0) {
                 float xv[4] = {hreg[j].x, hreg[j].y, hreg[j].z, hreg[j].w};
                 if constexpr (PRE::kind == 1) {
-                    if (hsrc[j]) {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            xv[e] = bn_bwd_elem(xv[e], f4get(yreg[j], e), cf[0][e], cf[1][e], cf[2][e], cf[3][e],
-                                                cf[4][e], cf[5][e], cf[6][e]);
-                    }
+                    for (int e = 0; e < 4; ++e)
+                        xv[e] = bn_bwd_elem(xv[e], f4get(yreg[j], e), cf[0][e], cf[1][e], cf[2][e], cf[3][e],
+                                            cf[4][e], cf[5][e], cf[6][e]);
                 } else if constexpr (PRE::kind == 2) {
-                    if (hsrc[j]) {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) xv[e] = bn_relu_elem(xv[e], cf[0][e], cf[1][e]);
-                    }
+                    for (int e = 0; e < 4; ++e) xv[e] = bn_relu_elem(xv[e], cf[0][e], cf[1][e]);
                 }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) xv[e] = hin[j] ? xv[e] : 0.f;   // zero padding (transform not applied)
                 __bf16 h[4], m[4], l[4];
                 if constexpr (ABL & 8) {
 #pragma unroll
@@ -962,29 +975,35 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     // two register sets for B: the groups dy = 1 and dy = 2 of a chunk are both fetched at the chunk's start,
     // ahead of the next chunk's halo, so the per-group B waits never wait for the (HBM-latency) halo loads:
     // the halo has the whole chunk (3 barrier intervals) to arrive (vmcnt counts in issue order)
-    uint4 bregA[BQ], bregB[BQ];
-    auto gload_b = [&](int g, uint4 (&breg)[BQ]) {
+    u32x4 bregA[BQ], bregB[BQ];
+    // unconditional loads (see the halo): a piece past the group loads an in-bounds dummy and is not stored; a
+    // column >= Cout (Cout % 128 != 0) loads a copy of column Cout - 1: its accumulators are never stored (a select
+    // here would be hoisted to the load by the scheduler and wait on it)
+    auto gload_b = [&](int g, u32x4 (&breg)[BQ]) {
 #pragma unroll
         for (int j = 0; j < BQ; ++j) {
             const int q = tid + j * HTHREADS;
-            const int pl = q >> 8, dx = pl / NS, t = pl - dx * NS, rr = (q & 255) >> 1, half = q & 1;
-            const int n = n0 + rr;
-            breg[j] = (q < BPL * 256 && n < Cout)
-                          ? *reinterpret_cast<const uint4*>(wx3 + (((long long)(g * 3 + dx) * 3 + t) * Cout + n) * XBK +
-                                                            half * 8)
-                          : make_uint4(0, 0, 0, 0);
+            const int pl = min(q >> 8, BPL - 1), dx = pl / NS, t = pl - dx * NS, half = q & 1;
+            const int n = min(n0 + ((q & 255) >> 1), Cout - 1);
+            breg[j] = *reinterpret_cast<const u32x4*>(wx3 + (((long long)(g * 3 + dx) * 3 + t) * Cout + n) * XBK +
+                                                      half * 8);
         }
     };
     int bstores = 0;
-    auto store_b = [&](__bf16* base, const uint4 (&breg)[BQ]) {
+    auto store_b = [&](int boff, const u32x4 (&breg)[BQ]) {   // into Bs + boff
         if constexpr (ABL & 4) {
             if (bstores++ >= 2) return;
         }
+        // an opaque offset: the compiler can no longer prove the stores disjoint from the current kernel row's
+        // fragment reads, so it keeps them after those reads instead of pulling them (and their load waits) up
+        // among the first MFMAs
+        asm volatile("" : "+s"(boff));
+        __bf16* base = Bs + boff;
 #pragma unroll
         for (int j = 0; j < BQ; ++j) {
             const int q = tid + j * HTHREADS;
             if (q < BPL * 256)
-                *reinterpret_cast<uint4*>(base + (q >> 8) * XPLANE + xoff((q & 255) >> 1, (q & 1) * 8)) = breg[j];
+                *reinterpret_cast<u32x4*>(base + (q >> 8) * XPLANE + xoff((q & 255) >> 1, (q & 1) * 8)) = breg[j];
         }
     };
 
@@ -1097,7 +1116,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     gload_halo(0);
     gload_b(0, bregA);
     store_halo(Hs, 0);
-    store_b(Bs, bregA);
+    store_b(0, bregA);
     __syncthreads();
     int hb = 0, bb = 0;
     for (int kt = 0, t = t_first; kt < tpb && t < mtiles; ++kt, t += t_step) {
@@ -1115,28 +1134,25 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         // dy = 0: fetch B of dy = 1 and dy = 2, then the next chunk's halo (or the next tile's first)
         gload_b(g0 + 1, bregA);
         gload_b(g0 + 2, bregB);
-        if (morec) {
-            gload_halo(cc + 1);
-        } else if (nextt) {
-            setup_tile(t + t_step);
-            gload_halo(0);
-        }
+        if (!morec && nextt) setup_tile(t + t_step);
+        gload_halo(morec ? cc + 1 : 0);   // (a dummy reload of chunk 0 after the block's last chunk)
         compute(0, a, Bs + bb * BPL * XPLANE);
-        store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregA);
+        store_b((bb ^ 1) * BPL * XPLANE, bregA);
         sync();
         bb ^= 1;
         // dy = 1
         compute(1, a, Bs + bb * BPL * XPLANE);
-        store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregB);
+        store_b((bb ^ 1) * BPL * XPLANE, bregB);
         sync();
         bb ^= 1;
         // dy = 2: fetch B of the next chunk's dy = 0; split + store the next halo (buffer idle since chunk cc-1)
         // ahead of this group's MFMAs, so its VALU work interleaves with them; B after them (just issued)
-        if (morec) gload_b(g0 + 3, bregA);
-        else if (nextt) gload_b(0, bregA);
-        if (morec) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
+        gload_b(morec ? g0 + 3 : 0, bregA);
+        const bool late = (ABL & 256) && wave < 4;   // staggered split: wave-uniform
+        if (morec && !late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
         compute(2, a, Bs + bb * BPL * XPLANE);
-        if (morec) store_b(Bs + (bb ^ 1) * BPL * XPLANE, bregA);
+        if (morec && late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
+        if (morec) store_b((bb ^ 1) * BPL * XPLANE, bregA);
         sync();
         bb ^= 1;
         hb ^= 1;
@@ -1146,7 +1162,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     if (nextt) {   // the next tile's chunk 0 (its loads were issued during the last chunk)
         __syncthreads();                 // the epilogue's scratch aliases the operand LDS
         store_halo(Hs + hb * NS * HPLANE, 0);
-        store_b(Bs + bb * BPL * XPLANE, bregA);
+        store_b(bb * BPL * XPLANE, bregA);
         __syncthreads();
     }
     }
@@ -1880,6 +1896,9 @@ CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int C
         case 62: CDM_ABL(62); break;
         case 65: CDM_ABL(65); break;
         case 129: CDM_ABL(129); break;
+        case 257: CDM_ABL(257); break;
+        case 513: CDM_ABL(513); break;
+        case 769: CDM_ABL(769); break;
         default: return (int)hipErrorInvalidValue;
     }
 #undef CDM_ABL

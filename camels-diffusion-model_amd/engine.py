@@ -132,6 +132,9 @@ class UNetEngine:
         self._amax = torch.zeros(2, device=self.device)     # h3: max|A|, max|B| of the current launch
         # h3 train: batched repack (3 launches per step); $CDM_BATCH_REPACK=0 keeps the per-layer launches (A/B)
         self.batch_repack = os.environ.get("CDM_BATCH_REPACK", "1") != "0"
+        # measurement hook: probe(args) before every 3x3 conv launch, args = the _conv3x3 arguments (bench.py replays
+        # the dominant conv's launches of a real train step on their real operands); None in production
+        self.launch_probe = None
         self._batch_key = None
 
     # ------------------------------------------------------------------------------------------
@@ -267,6 +270,14 @@ class UNetEngine:
         amax_y = slot that receives max|y| for the next conv; pre = (scale, shift) pointers: the input is
         relu(x * scale + shift) of the previous layer's pre-norm output, applied while staging; ymm = (ptr, ld):
         per-channel max / min keys of y for the next layer's fused apply."""
+        args = (key, x_p, B, S, cin, ldx, bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, s, amax_x, amax_y,
+                pre, ymm)
+        if self.launch_probe is not None:
+            self.launch_probe(args)
+        self._conv3x3(*args)
+
+    def _conv3x3(self, key, x_p, B, S, cin, ldx, bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, s, amax_x,
+                 amax_y, pre, ymm):
         if self.nterm == NT_H3:
             if amax_x is None:
                 assert pre is None
@@ -305,8 +316,8 @@ class UNetEngine:
 
     def fuses_bn_bwd(self, l: "LayerSpec", kind: str) -> bool:
         """Layer l's BN backward runs inside its dgrad / wgrad staging (cdm_conv3x3_*_h3_bnbwd)."""
-        return (self.fuse_bn_bwd and kind == "dense" and l.cin > 1 and l.S in (32, 64, 128) and l.kc == 16
-                and l.cin % 128 == 0 and l.cout % 128 == 0 and l.cout <= 256)
+        return (self.fuse_bn_bwd and kind in ("dense", "plain", "resid") and l.cin > 1 and l.S in (32, 64, 128)
+                and l.kc == 16 and l.cin % 128 == 0 and l.cout % 128 == 0 and l.cout <= 256)
 
     # h3 operand maxima: one device slot per producer, zeroed at the start of every forward --------------
     def _slot(self, ws, key):
@@ -544,7 +555,8 @@ class UNetEngine:
         self._wgrad3x3(ws, Act(dyO, nf), ws.catO, B, H, 2 * nf, nf, G["out.0.weight"], s, amax_dy=dslot,
                        amax_x=self._slot(ws, "catO"))
         self.conv3x3("out.0.wdg", _p(dyO), B, H, nf, nf, None, ws.dcatO.p, ws.dcatO.ld, 2 * nf, 0, None, 0,
-                     self.kc_out0, s, amax_x=dslot)
+                     self.kc_out0, s, amax_x=dslot,
+                     amax_y=self._slot(ws, ws.out0_g_key) if ws.out0_g_key else None)
         hook("out")
         # ---------------- up2 blocks ----------------
         self._chain_bwd(ws, P, self.layers[14:18], G, s)
@@ -922,7 +934,7 @@ class Workspace:
                     self.dgrad_dst[l.name], self.dgrad_accum[l.name] = Act(Gb, l.cin), False
             self._wire_fused_bn_bwd(eng, L, kinds)
         else:
-            self.fused, self.g_amax_key = set(), {}
+            self.fused, self.g_amax_key, self.out0_g_key = set(), {}, None
 
     def ymm_of(self, l) -> tuple:
         """(pointer, ld) of fused layer l's max keys; its min keys sit ld ints further."""
@@ -936,6 +948,7 @@ class Workspace:
         (in place when their g already sits in D: the mode-0 apply is elementwise, index for index)."""
         self.fused = {l.name for l in L if eng.fuses_bn_bwd(l, kinds[l.name])}
         self.g_amax_key = {}
+        self.out0_g_key = None
         if not self.fused:
             return
         other = {}
@@ -945,12 +958,16 @@ class Workspace:
         for l in reversed(L):
             if l.name not in self.fused:
                 continue
-            nxt = L[idx[l.name] + 1]                      # its g is written by the next layer's dgrad
-            self.g_amax_key[nxt.name] = "g:" + l.name
+            if idx[l.name] + 1 < len(L):
+                nxt = L[idx[l.name] + 1]                  # its g is written (last) by the next layer's dgrad
+                self.g_amax_key[nxt.name] = "g:" + l.name
+            else:                                         # up2's last conv ("plain"): g is out.0's dgrad output
+                self.out0_g_key = "g:" + l.name
             g = self.gout[l.name]
             if l.name in ("down1.model.0.conv1", "down2.model.0.conv1"):
                 continue                                  # dgrad accumulates into a concat-grad slice
-            dst = other[g.buf.data_ptr()]
+            # g of a "plain" / "resid" layer is a slice of the concat gradient: any buffer of the pair is free
+            dst = other.get(g.buf.data_ptr(), self.G0 if l.S == self.eng.H else self.G1)
             self.dgrad_dst[l.name] = Act(dst, l.cin)
             if l.name == "up1.model.1.conv1":
                 self.gT1 = dst

@@ -233,7 +233,7 @@ class Trainer:
         self.graph = g
 
     def step(self, x0: Optional[torch.Tensor] = None, c: Optional[torch.Tensor] = None, inject=None,
-             global_count: Optional[int] = None) -> torch.Tensor:
+             global_count: Optional[int] = None, eager: bool = False) -> torch.Tensor:
         """One training step on batch (x0 [B,1,H,H] in [0,1], c [B, n_cfeat] or None = unconditional).
 
         ``inject=(noise [B,1,H,H], t [B] int, shortcut [2*n_feat] = weight|bias)`` replaces the on-device
@@ -255,7 +255,7 @@ class Trainer:
         if self.ddp and self.broadcast_buffers:
             import torch.distributed as dist
             dist.broadcast(self.bnflat, 0, group=self.group)
-        if self.use_graph and inject is None and B == self.B and self.grad_numel is None:
+        if self.use_graph and inject is None and B == self.B and self.grad_numel is None and not eager:
             if self.graph is None:
                 self._body(_s())          # eager warm-up step (loads every kernel) then capture
                 self._capture()

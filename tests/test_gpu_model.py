@@ -223,7 +223,8 @@ def test_fused_bn_bwd_matches_unfused_nf128():
             F.mse_loss(pred, noise.cuda()).backward()
             grads.append({k: p.grad.detach().double().cpu() for k, p in m.named_parameters()})
             if fuse:
-                assert len(eng.workspace(B, True).fused) == 12     # the dense-kind 128/256-ch BN layers, C_in > 1
+                # the 128/256-ch BN layers with C_in > 1 whose apply is a plain BN-ReLU (dense, plain, resid)
+                assert len(eng.workspace(B, True).fused) == 14
     finally:
         eng.fuse_bn_bwd = True
         M._WS.clear()

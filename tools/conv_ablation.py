@@ -40,7 +40,9 @@ def main(B=256, H=64, C=128, reps=10, relu=True):
     prod = lambda: L.cdm_conv3x3_fwd_h3(x.data_ptr(), B, H, H, C, C, wx.data_ptr(), am.data_ptr(), am.data_ptr() + 4,
                                         b.data_ptr(), y.data_ptr(), C, C, 0, st.data_ptr(), C, 16, None, s)
     fns = {"prod": prod}
-    for abl in (1, 1 | 2 << 16, 1 | 4 << 16, 1 | 8 << 16, 1 | 16 << 16, 61):
+    abls = [int(a) for a in os.environ.get("CDM_ABLS", "").split(",") if a] or [1, 1 | 2 << 16, 1 | 4 << 16,
+                                                                               1 | 8 << 16, 1 | 16 << 16, 61]
+    for abl in abls:
         fns[abl] = (lambda abl=abl: L.cdm_conv3x3_halo_ablate(
             abl, x.data_ptr(), B, H, C, C, wx.data_ptr(), am.data_ptr(), am.data_ptr() + 4, y.data_ptr(), C, C, s))
     for f in fns.values():
