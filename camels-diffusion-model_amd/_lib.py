@@ -98,11 +98,12 @@ def lib() -> _Lib:
     if _inst is None:
         with _lock:
             if _inst is None:
-                if not os.path.exists(LIBPATH):
+                path = os.environ.get("CDM_LIB") or LIBPATH   # A/B timing of two builds (tools); unset in the product
+                if not os.path.exists(path):
                     raise RuntimeError(
-                        f"libcdm_hip.so not found at {LIBPATH}; build it with "
+                        f"libcdm_hip.so not found at {path}; build it with "
                         "`python camels-diffusion-model_amd/build.py` (or __graft_entry__.build())")
-                _inst = _Lib(LIBPATH)
+                _inst = _Lib(path)
     return _inst
 
 

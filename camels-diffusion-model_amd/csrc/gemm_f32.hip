@@ -18,6 +18,7 @@
 // loaders (zero fill) and the epilogues (masked stores), so any M and N%4==0, K%4==0 work.
 #include "cdm_common.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace cdm {
 
@@ -842,8 +843,12 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
                                                                       int mtiles, int tpb) {
     constexpr int NS = XTerms<NT>::NS;
     constexpr int ROWS = HBM_ / WT, HR = ROWS + 2, HC = WT + 2, HPX = HR * HC;
-    constexpr int HPLANE = HPX * XBK;                 // bf16 per halo term plane
     constexpr int HQ = (HPX * 4 + HTHREADS - 1) / HTHREADS;   // float4 halo pieces per thread
+    // halo planes padded to HQ x 512 pieces where LDS allows: every piece then has a slot (past-the-halo pieces
+    // write unused padding), so the split + store has no branches and can share a scheduling region with MFMAs
+    constexpr int HPXA = HQ * HTHREADS / 4;
+    constexpr bool HPAD = (2 * NS * HPXA * XBK + 2 * 3 * NS * XPLANE) * 2 + 7 * 256 * 4 <= 160 * 1024;
+    constexpr int HPLANE = (HPAD ? HPXA : HPX) * XBK;   // bf16 per halo term plane
     constexpr int BPL = 3 * NS;                       // B planes per group (3 taps x NS terms)
     constexpr int BQ = (BPL * 256 + HTHREADS - 1) / HTHREADS;  // 16-byte B pieces per thread
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * NS * HPLANE + 2 * BPL * XPLANE];
@@ -915,7 +920,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 #pragma unroll
     for (int j = 0; j < HQ; ++j) {
         const int q = tid + j * HTHREADS;
-        hdst[j] = q < HPX * 4 ? xoff(q >> 2, (q & 3) * 4) : -1;
+        hdst[j] = (HPAD || q < HPX * 4) ? xoff(q >> 2, (q & 3) * 4) : -1;
     }
     setup_tile(t_first);
     auto gload_halo = [&](int cc) {
@@ -940,7 +945,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         }
 #pragma unroll
         for (int j = 0; j < HQ; ++j) {
-            if (hdst[j] >= 0) {
+            if (HPAD || hdst[j] >= 0) {
                 float xv[4] = {hreg[j].x, hreg[j].y, hreg[j].z, hreg[j].w};
                 if constexpr (PRE::kind == 1) {
 #pragma unroll
@@ -979,15 +984,20 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     // unconditional loads (see the halo): a piece past the group loads an in-bounds dummy and is not stored; a
     // column >= Cout (Cout % 128 != 0) loads a copy of column Cout - 1: its accumulators are never stored (a select
     // here would be hoisted to the load by the scheduler and wait on it)
-    auto gload_b = [&](int g, u32x4 (&breg)[BQ]) {
+    // per-lane byte offsets of the pieces within a group (fixed per block); the group offset is uniform, so each
+    // load is a scalar-base + 32-bit lane-offset address (no 64-bit multiplies in the loop)
+    unsigned bpo[BQ];
 #pragma unroll
-        for (int j = 0; j < BQ; ++j) {
-            const int q = tid + j * HTHREADS;
-            const int pl = min(q >> 8, BPL - 1), dx = pl / NS, t = pl - dx * NS, half = q & 1;
-            const int n = min(n0 + ((q & 255) >> 1), Cout - 1);
-            breg[j] = *reinterpret_cast<const u32x4*>(wx3 + (((long long)(g * 3 + dx) * 3 + t) * Cout + n) * XBK +
-                                                      half * 8);
-        }
+    for (int j = 0; j < BQ; ++j) {
+        const int q = tid + j * HTHREADS;
+        const int pl = min(q >> 8, BPL - 1), dx = pl / NS, t = pl - dx * NS, half = q & 1;
+        const int n = min(n0 + ((q & 255) >> 1), Cout - 1);
+        bpo[j] = (unsigned)(((dx * 3 + t) * Cout + n) * XBK + half * 8) * 2u;
+    }
+    auto gload_b = [&](int g, u32x4 (&breg)[BQ]) {
+        const char* gb = reinterpret_cast<const char*>(wx3) + (long long)g * (9 * XBK * 2) * Cout;
+#pragma unroll
+        for (int j = 0; j < BQ; ++j) breg[j] = *reinterpret_cast<const u32x4*>(gb + bpo[j]);
     };
     int bstores = 0;
     auto store_b = [&](int boff, const u32x4 (&breg)[BQ]) {   // into Bs + boff
@@ -1032,7 +1042,19 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         else return xmfma<NT>(fa_, fb_, c_);
     };
     // the 3 taps (dx) of kernel row dy of the current chunk: fragments from the halo image a and B group b
-    auto compute = [&](int dy, const __bf16* a, const __bf16* b) {
+    // vtag = std::integral_constant<int, V>: V > 0 interleaves V VALU instructions (and a DS write every 4th MFMA)
+    // into every MFMA gap — the halo split of the next chunk, placed in the same scheduling region (ABL 1024)
+    auto compute = [&](int dy, const __bf16* a, const __bf16* b, auto vtag) {
+        constexpr int V = decltype(vtag)::value;
+        int nmf = 0;
+        auto mf1 = [&]() {   // one MFMA slot of the pinned schedule
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if constexpr (V > 0) {
+                __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+                // the LDS writes after the last fragment read (they may alias it): in the last tap
+                if (++nmf > 24 && (nmf & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+            }
+        };
         // register double buffer: the fragments of tap dx+1 are read while the MFMAs of tap dx issue
         bf16x8 FA[2][2][NS], FB[2][2][NS];
         auto ldfrag = [&](int buf, int dx) {
@@ -1083,6 +1105,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         if constexpr (PREFETCH) {
             // pin the interleave: the next tap's fragment reads go one per MFMA gap of the current tap
             constexpr int MF = 4 * (NT >= 6 ? 6 : (NT >= 3 ? 3 : 1)), RD = 4 * NS;
+            if constexpr (V > 0) __builtin_amdgcn_sched_group_barrier(0x020, BQ, 0);   // next B loads first
             __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);          // tap 0 fragments
 #pragma unroll
             for (int dx = 0; dx < 2; ++dx) {
@@ -1100,15 +1123,27 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
                 } else {
 #pragma unroll
                     for (int k = 0; k < RD; ++k) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        mf1();
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     }
-                    __builtin_amdgcn_sched_group_barrier(0x008, MF - RD, 0);
+                    if constexpr (V > 0) {
+#pragma unroll
+                        for (int k = 0; k < MF - RD; ++k) mf1();
+                    } else {
+                        __builtin_amdgcn_sched_group_barrier(0x008, MF - RD, 0);
+                    }
                 }
             }
-            __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);          // last tap
+            if constexpr (V > 0) {                                        // last tap
+#pragma unroll
+                for (int k = 0; k < MF; ++k) mf1();
+            } else {
+                __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);
+            }
         }
     };
+    using V0 = std::integral_constant<int, 0>;
+    using VH = std::integral_constant<int, (ABL & 1024) ? 4 : 0>;
 
     auto sync = [&]() {
         if constexpr (!(ABL & 16)) __syncthreads();
@@ -1136,12 +1171,12 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         gload_b(g0 + 2, bregB);
         if (!morec && nextt) setup_tile(t + t_step);
         gload_halo(morec ? cc + 1 : 0);   // (a dummy reload of chunk 0 after the block's last chunk)
-        compute(0, a, Bs + bb * BPL * XPLANE);
+        compute(0, a, Bs + bb * BPL * XPLANE, V0{});
         store_b((bb ^ 1) * BPL * XPLANE, bregA);
         sync();
         bb ^= 1;
         // dy = 1
-        compute(1, a, Bs + bb * BPL * XPLANE);
+        compute(1, a, Bs + bb * BPL * XPLANE, V0{});
         store_b((bb ^ 1) * BPL * XPLANE, bregB);
         sync();
         bb ^= 1;
@@ -1149,8 +1184,16 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         // ahead of this group's MFMAs, so its VALU work interleaves with them; B after them (just issued)
         gload_b(morec ? g0 + 3 : 0, bregA);
         const bool late = (ABL & 256) && wave < 4;   // staggered split: wave-uniform
-        if (morec && !late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
-        compute(2, a, Bs + bb * BPL * XPLANE);
+        if constexpr (!(ABL & 1024)) {
+            if (morec && !late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
+        }
+        compute(2, a, Bs + bb * BPL * XPLANE, VH{});
+        if constexpr (ABL & 1024) {
+            // after the MFMAs in program order (its LDS writes may alias the fragment reads) but in their scheduling
+            // region: the split's VALU fills the MFMA gaps; unconditional — after the block's last chunk it writes
+            // the idle buffer, which the next tile's chunk 0 overwrites after the epilogue
+            store_halo(Hs + (hb ^ 1) * NS * HPLANE, morec ? cc + 1 : 0);
+        }
         if (morec && late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
         if (morec) store_b((bb ^ 1) * BPL * XPLANE, bregA);
         sync();
@@ -1899,6 +1942,7 @@ CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int C
         case 257: CDM_ABL(257); break;
         case 513: CDM_ABL(513); break;
         case 769: CDM_ABL(769); break;
+        case 1025: CDM_ABL(1025); break;
         default: return (int)hipErrorInvalidValue;
     }
 #undef CDM_ABL

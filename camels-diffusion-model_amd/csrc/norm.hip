@@ -227,30 +227,39 @@ __global__ void bn_eval_coeffs_kernel(int C, const float* gamma, const float* be
 }
 
 // GroupNorm: block per image n; partials slab[n][nchunks][R][C].
-__global__ void gn_fwd_finalize_kernel(const float* slab, int nchunks, int R, int C, int G, double count,
-                                       const float* gamma, const float* beta, float eps, float* mean,
+// one block per (sample n, group g): the group's (chunk, channel) partials strided over 256 threads, fp64, then a
+// fixed-order tree (deterministic).  (One thread per group walking every chunk took ~1 ms per launch at C5's
+// 256^2 maps: 512 chunks x 8 channels serially, 16 blocks.)
+__global__ __launch_bounds__(256) void gn_fwd_finalize_kernel(const float* slab, int nchunks, int R, int C, int G,
+                                       double count, const float* gamma, const float* beta, float eps, float* mean,
                                        float* invstd, float* scale, float* shift) {
-    const int n = blockIdx.x;
+    const int n = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
     const int cpg = C / G;
-    __shared__ float sm[64], si[64];
-    for (int g = threadIdx.x; g < G; g += blockDim.x) {
-        double s = 0.0, q = 0.0;
-        for (int k = 0; k < nchunks; ++k)
-            for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
-                s += slab[(((long long)n * nchunks + k) * R + 0) * C + c];
-                q += slab[(((long long)n * nchunks + k) * R + 1) * C + c];
-            }
-        const double mu = s / count;
-        double var = q / count - mu * mu;
+    __shared__ double rs[256], rq[256];
+    __shared__ float sm, si;
+    double s = 0.0, q = 0.0;
+    for (int i = tid; i < nchunks * cpg; i += 256) {
+        const int k = i / cpg, c = g * cpg + (i - k * cpg);
+        const float* p = slab + (((long long)n * nchunks + k) * R) * C + c;
+        s += p[0]; q += p[C];
+    }
+    rs[tid] = s; rq[tid] = q;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) { rs[tid] += rs[tid + o]; rq[tid] += rq[tid + o]; }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const double mu = rs[0] / count;
+        double var = rq[0] / count - mu * mu;
         if (var < 0.0) var = 0.0;
-        sm[g] = (float)mu; si[g] = (float)(1.0 / sqrt(var + (double)eps));
-        mean[n * G + g] = sm[g]; invstd[n * G + g] = si[g];
+        sm = (float)mu; si = (float)(1.0 / sqrt(var + (double)eps));
+        mean[n * G + g] = sm; invstd[n * G + g] = si;
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        const int g = c / cpg;
-        const float sc = gamma[c] * si[g];
-        scale[n * C + c] = sc; shift[n * C + c] = beta[c] - sm[g] * sc;
+    for (int c = g * cpg + tid; c < (g + 1) * cpg; c += 256) {
+        const float sc = gamma[c] * si;
+        scale[n * C + c] = sc; shift[n * C + c] = beta[c] - sm * sc;
     }
 }
 
@@ -284,32 +293,43 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* part
 
 // GroupNorm backward: block per image n. Writes per-(n,c) coefficients and per-(n,c) parameter
 // partials pdg/pdb/pdbias[n][c] (summed over n by a follow-up column reduction) and FiLM sums.
-__global__ void gn_bwd_finalize_kernel(const float* slab, int nchunks, int C, int G, double count_g, int HW,
-                                       const float* gamma, const float* invstd, float* A, float* B, float* Cc,
-                                       float* pdg, float* pdb, float* pdbias) {
-    const int n = blockIdx.x, cpg = C / G;
-    __shared__ double sdx[64], sdxx[64];
-    for (int g = threadIdx.x; g < G; g += blockDim.x) {
-        double a1 = 0.0, a2 = 0.0;
-        for (int k = 0; k < nchunks; ++k) {
-            const float* p = slab + ((long long)n * nchunks + k) * 5 * C;
-            for (int c = g * cpg; c < (g + 1) * cpg; ++c) { a1 += (double)gamma[c] * p[c]; a2 += (double)gamma[c] * p[C + c]; }
+// one block per (sample n, group g) as the forward finalize: thread t sums channel g*cpg + t % cpg over the chunks
+// t / cpg, t / cpg + 256 / cpg, ... (fp64); the per-channel sums are then folded in thread order (deterministic),
+// and the group sums sum_c gamma_c * (channel sum) follow from them.
+__global__ __launch_bounds__(256) void gn_bwd_finalize_kernel(const float* slab, int nchunks, int C, int G,
+                                       double count_g, int HW, const float* gamma, const float* invstd, float* A,
+                                       float* B, float* Cc, float* pdg, float* pdb, float* pdbias) {
+    const int n = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, cpg = C / G;
+    __shared__ double r1[256], r2[256], r5[256];
+    __shared__ double ch1[64], ch2[64], ch5[64], gs[2];
+    const int per = 256 / cpg;                      // threads per channel (cpg <= 64: launch check)
+    const int cl = tid % cpg, c = g * cpg + cl;
+    double s1 = 0.0, s2 = 0.0, s5 = 0.0;
+    if (tid < per * cpg)
+        for (int k = tid / cpg; k < nchunks; k += per) {
+            const float* p = slab + ((long long)n * nchunks + k) * 5 * C + c;
+            s1 += p[0]; s2 += p[C]; s5 += p[4 * C];
         }
-        sdx[g] = a1; sdxx[g] = a2;
+    r1[tid] = s1; r2[tid] = s2; r5[tid] = s5;
+    __syncthreads();
+    if (tid < cpg) {
+        double a = 0.0, b = 0.0, e = 0.0;
+        for (int j = 0; j < per; ++j) { a += r1[j * cpg + tid]; b += r2[j * cpg + tid]; e += r5[j * cpg + tid]; }
+        ch1[tid] = a; ch2[tid] = b; ch5[tid] = e;
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        const int g = c / cpg;
-        double s1 = 0.0, s2 = 0.0, s5 = 0.0;
-        for (int k = 0; k < nchunks; ++k) {
-            const float* p = slab + ((long long)n * nchunks + k) * 5 * C;
-            s1 += p[c]; s2 += p[C + c]; s5 += p[4 * C + c];
-        }
+    if (tid == 0) {
+        double a1 = 0.0, a2 = 0.0;
+        for (int j = 0; j < cpg; ++j) { a1 += (double)gamma[g * cpg + j] * ch1[j]; a2 += (double)gamma[g * cpg + j] * ch2[j]; }
+        gs[0] = a1; gs[1] = a2;
+    }
+    __syncthreads();
+    if (tid < cpg) {
         const double is = invstd[n * G + g];
-        const double a = (double)gamma[c] * is, b = -is * sdx[g] / count_g, cc = -is * sdxx[g] / count_g;
+        const double a = (double)gamma[c] * is, b = -is * gs[0] / count_g, cc = -is * gs[1] / count_g;
         A[n * C + c] = (float)a; B[n * C + c] = (float)b; Cc[n * C + c] = (float)cc;
-        pdg[n * C + c] = (float)s2; pdb[n * C + c] = (float)s1;
-        pdbias[n * C + c] = (float)(a * s1 + b * (double)HW + cc * s5);
+        pdg[n * C + c] = (float)ch2[tid]; pdb[n * C + c] = (float)ch1[tid];
+        pdbias[n * C + c] = (float)(a * ch1[tid] + b * (double)HW + cc * ch5[tid]);
     }
 }
 
@@ -559,8 +579,9 @@ CDM_API int cdm_gn_fwd_finalize(const float* slab, int N, int nchunks, int R, in
                                 const float* gamma, const float* beta, float eps, float* mean, float* invstd,
                                 float* scale, float* shift, void* stream) {
     if (G > 64) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(gn_fwd_finalize_kernel, dim3(N), dim3(256), 0, S(stream), slab, nchunks, R, C, G, count, gamma,
-                       beta, eps, mean, invstd, scale, shift);
+    if (C % G) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(gn_fwd_finalize_kernel, dim3(N, G), dim3(256), 0, S(stream), slab, nchunks, R, C, G, count,
+                       gamma, beta, eps, mean, invstd, scale, shift);
     return cdm_status();
 }
 
@@ -575,9 +596,9 @@ CDM_API int cdm_bn_bwd_finalize(const double* part, int nparts, int C, double co
 CDM_API int cdm_gn_bwd_finalize(const float* slab, int N, int nchunks, int C, int G, double count_g, int HW,
                                 const float* gamma, const float* invstd, float* A, float* B, float* Cc, float* pdg,
                                 float* pdb, float* pdbias, void* stream) {
-    if (G > 64) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(N), dim3(256), 0, S(stream), slab, nchunks, C, G, count_g, HW, gamma,
-                       invstd, A, B, Cc, pdg, pdb, pdbias);
+    if (C % G || C / G > 64) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(N, G), dim3(256), 0, S(stream), slab, nchunks, C, G, count_g, HW,
+                       gamma, invstd, A, B, Cc, pdg, pdb, pdbias);
     return cdm_status();
 }
 
