@@ -11,7 +11,7 @@ mkdir -p $R/camels-diffusion-model_amd/lib/ab
 objs=""
 for f in $T/camels-diffusion-model_amd/csrc/*.hip; do
   o=$T/$(basename $f).o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I $T/camels-diffusion-model_amd/csrc -I $T/include -Wno-unused-result -c $f -o $o &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $EXTRA -I $T/camels-diffusion-model_amd/csrc -I $T/include -Wno-unused-result -c $f -o $o &
   objs="$objs $o"
 done
 wait
