@@ -897,12 +897,15 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     // them and waits for vmcnt(0) — the B stores of a kernel row then waited on the next chunk's halo (HBM latency)
     // and the halo split on the B loads just issued.
     float4 hreg[HQ];
-    const float* hsrc[HQ];          // chunk-0 source of piece j (a dummy in-bounds address when !hin[j])
+    // chunk-0 source of piece j as a 32-bit byte offset from the uniform base x (pre.y): scalar base + lane offset
+    // loads, one VGPR per piece instead of a 64-bit pointer (the PreBnBwd variant spilled with two pointers per piece).
+    // Offsets stay below 2^32: the host checks N H W ldx * 4 bytes < 2^32 (cdm_conv3x3 entry points).
+    unsigned hxo[HQ];               // (a dummy in-bounds offset 0 + channel quad when !hin[j])
     bool hin[HQ];                   // piece j is inside the image (else zero padding / past the halo)
     int hdst[HQ];                   // its LDS offset within a term plane
     float4 yreg[PRE::on ? HQ : 1];  // PreBnBwd: the pre-norm activations of piece j
-    const float* hysrc[PRE::on ? HQ : 1];
-    auto setup_tile = [&](int t) {  // halo source addresses of tile t
+    unsigned hyo[PRE::on ? HQ : 1];
+    auto setup_tile = [&](int t) {  // halo source offsets of tile t
         const int m0 = t * HBM_, img = m0 / hw, h0 = (m0 - img * hw) / WT;
 #pragma unroll
         for (int j = 0; j < HQ; ++j) {
@@ -911,10 +914,10 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
             const int hr = hp / HC, hc = hp - hr * HC;
             const int ih = h0 - 1 + hr, iw = hc - 1;
             const bool in = q < HPX * 4 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)WT;
-            const long long pix = in ? (long long)(img * H + ih) * WT + iw : 0;
+            const unsigned pix = in ? (unsigned)((img * H + ih) * WT + iw) : 0u;
             hin[j] = in;
-            hsrc[j] = x + pix * ldx + c4 * 4;
-            if constexpr (PRE::on) hysrc[j] = pre.y + pix * pre.ldy + c4 * 4;
+            hxo[j] = (pix * (unsigned)ldx + (unsigned)c4 * 4u) * 4u;
+            if constexpr (PRE::on) hyo[j] = (pix * (unsigned)pre.ldy + (unsigned)c4 * 4u) * 4u;
         }
     };
 #pragma unroll
@@ -927,10 +930,13 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         if constexpr (ABL & 32) {
             if (cc > 0) return;
         }
+        const char* xb = reinterpret_cast<const char*>(x + cc * 16);
 #pragma unroll
-        for (int j = 0; j < HQ; ++j) {
-            hreg[j] = ld4(hsrc[j] + cc * 16);
-            if constexpr (PRE::on) yreg[j] = ld4(hysrc[j] + cc * 16);
+        for (int j = 0; j < HQ; ++j) hreg[j] = *reinterpret_cast<const float4*>(xb + hxo[j]);
+        if constexpr (PRE::on) {
+            const char* yb = reinterpret_cast<const char*>(pre.y + cc * 16);
+#pragma unroll
+            for (int j = 0; j < HQ; ++j) yreg[j] = *reinterpret_cast<const float4*>(yb + hyo[j]);
         }
     };
     auto store_halo = [&](__bf16* base, int cc) {
@@ -1591,6 +1597,11 @@ static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, cons
                             const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm, hipStream_t s,
                             PRE pre = PRE{}, int tpb = 0) {
     const int M = N * H * WT, mtiles = M / HBM_;
+    // the kernel addresses the halo sources (x, pre.y) by 32-bit byte offsets from their base
+    if ((unsigned long long)M * (unsigned)ldx * 4ull >= (1ull << 32)) return (int)hipErrorInvalidValue;
+    if constexpr (PRE::kind == 1) {
+        if ((unsigned long long)M * (unsigned)pre.ldy * 4ull >= (1ull << 32)) return (int)hipErrorInvalidValue;
+    }
     if (tpb < 1) tpb = halo_tpb(mtiles, (Cout + GBN - 1) / GBN, nterm, WT);
     dim3 grid((mtiles + tpb - 1) / tpb, (Cout + GBN - 1) / GBN, 1);
     if constexpr (WT > 64) {
@@ -1883,7 +1894,8 @@ static int conv3x3_fwd_split(const float* x, int N, int H, int W, int Cin, int l
     const int M = N * H * W, K = 9 * Cin;
     MkPre mb{reinterpret_cast<const __bf16*>(wx), Cout, amax_w};
     EpiStore ep{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
-    const bool halo = kc == 16 && W == H && halo_width_ok(W, nterm) && ldx % 4 == 0 && (H * W) % HBM_ == 0;
+    const bool halo = kc == 16 && W == H && halo_width_ok(W, nterm) && ldx % 4 == 0 && (H * W) % HBM_ == 0 &&
+                      (unsigned long long)M * (unsigned)ldx * 4ull < (1ull << 32);   // 32-bit halo source offsets
     if ((pre_s || ymm) && (!halo || (ymm && !stats) || (pre_s && (!pre_t || Cin > 256))))
         return (int)hipErrorInvalidValue;      // the fused BN-ReLU input / max-min epilogue: LDS-halo path only
     if (halo) {   // LDS-halo path
@@ -1915,6 +1927,7 @@ CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int C
                                     void* stream) {
     if (H != 64 || Cin % 16 || ldx % 4) return (int)hipErrorInvalidValue;
     const int M = N * H * 64, mtiles = M / HBM_;
+    if ((unsigned long long)M * (unsigned)ldx * 4ull >= (1ull << 32)) return (int)hipErrorInvalidValue;
     const int tpb = (abl >> 16) > 0 ? (abl >> 16) : 1;   // tiles per block in the high bits (0 -> 1)
     abl &= 0xffff;
     const EpiStoreW<4> eh{y, ldy, 0, nullptr, Cout, 0, nullptr, 0, M, Cout};

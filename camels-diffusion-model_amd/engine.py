@@ -300,11 +300,18 @@ class UNetEngine:
             lib().cdm_conv3x3_fwd(x_p, B, S, S, cin, ldx, _p(self.pk[key]), bias_p, y_p, ldy, cout, flags, stats_p,
                                   stats_ld, kc, s)
 
-    def fuses_bn_fwd(self, l: "LayerSpec", kind: str) -> bool:
+    def halo_addressable(self, B: int, S: int) -> bool:
+        """The LDS-halo conv addresses its sources by 32-bit byte offsets: B*S*S pixels x the widest row of any
+        activation / gradient buffer at that resolution (2 n_feat floats; 4 n_feat at H/4, catU1) must stay below
+        4 GiB for the fused (halo-only) paths."""
+        ld = (4 if S == self.H // 4 else 2) * self.nf
+        return B * S * S * ld * 4 < 2 ** 32
+
+    def fuses_bn_fwd(self, l: "LayerSpec", kind: str, B: int = 1) -> bool:
         """Producer l's train-mode BatchNorm apply (z = relu(y s + t)) runs inside the staging of the next conv (its
         forward and its weight gradient): z is never written.  Needs the LDS-halo path for both convs (max / min
         epilogue on l, BN-ReLU staging on the consumer) and the kernel-row weight gradient for the consumer."""
-        if not (self.fuse_bn_fwd and kind == "dense" and l.cin > 1):
+        if not (self.fuse_bn_fwd and kind == "dense" and l.cin > 1 and self.halo_addressable(B, l.S)):
             return False
         i = self.layers.index(l)
         if i + 1 >= len(self.layers):
@@ -314,9 +321,10 @@ class UNetEngine:
         return (halo(l) and halo(c) and c.cin == l.cout and c.cin <= 256 and c.cin % 128 == 0 and c.cout % 128 == 0
                 and c.S == l.S)
 
-    def fuses_bn_bwd(self, l: "LayerSpec", kind: str) -> bool:
+    def fuses_bn_bwd(self, l: "LayerSpec", kind: str, B: int = 1) -> bool:
         """Layer l's BN backward runs inside its dgrad / wgrad staging (cdm_conv3x3_*_h3_bnbwd)."""
         return (self.fuse_bn_bwd and kind in ("dense", "plain", "resid") and l.cin > 1 and l.S in (32, 64, 128)
+                and self.halo_addressable(B, l.S)
                 and l.kc == 16 and l.cin % 128 == 0 and l.cout % 128 == 0 and l.cout <= 256)
 
     # h3 operand maxima: one device slot per producer, zeroed at the start of every forward --------------
@@ -857,7 +865,7 @@ class Workspace:
         kinds["up1.model.2.conv2"] = "film"
         kinds["up2.model.2.conv2"] = "plain"
         self.dst_kind = kinds
-        self.fused_fwd = {l.name for l in L if train and eng.fuses_bn_fwd(l, kinds[l.name])}
+        self.fused_fwd = {l.name for l in L if train and eng.fuses_bn_fwd(l, kinds[l.name], B)}
         for l in L:
             k = kinds[l.name]
             if k == "dense":
@@ -946,7 +954,7 @@ class Workspace:
         must differ: walking the backward order, each fused layer writes its dgrad into the other buffer of its
         resolution's pair (G, D), which becomes the g of the layer before it.  Non-fused layers keep dy in D
         (in place when their g already sits in D: the mode-0 apply is elementwise, index for index)."""
-        self.fused = {l.name for l in L if eng.fuses_bn_bwd(l, kinds[l.name])}
+        self.fused = {l.name for l in L if eng.fuses_bn_bwd(l, kinds[l.name], self.B)}
         self.g_amax_key = {}
         self.out0_g_key = None
         if not self.fused:
