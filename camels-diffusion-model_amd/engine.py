@@ -124,6 +124,9 @@ class UNetEngine:
         self.layers = conv_layers(n_feat, height)
         self.L = {l.name: l for l in self.layers}
         self.KK0 = (height // 4) ** 2
+        # up0 on large maps (config 5: k = 64, 1.07 G weights): VALU kernels over the weights in their reference layout
+        # (cdm_up0_fwd / cdm_up0_wgrad) and one W^T for the input gradient, instead of two 4.3 GB repacks per step
+        self.up0_large = self.KK0 >= 1024 and self.KK0 % 256 == 0 and (2 * n_feat) % 16 == 0 and 2 * n_feat <= 512
         self.kc_out0 = conv_kc(2 * n_feat, n_feat)
         self.pk: Dict[str, torch.Tensor] = {}
         self._pk_key = None
@@ -224,10 +227,17 @@ class UNetEngine:
                 if train:
                     self._split(name + ".wtT", 4 * nf, cin, stream)
         c0 = 2 * nf
-        w0 = self._buf("up0.wt", (c0, self.KK0 * c0))
-        w0T = self._buf("up0.wtT", (self.KK0 * c0, c0))
-        lb.cdm_pack_convT(_p(P["up0.0.weight"]), c0, c0, self.KK0, _p(w0), _p(w0T) if train else None, stream)
-        self.pk["up0.wt"], self.pk["up0.wtT"] = w0, w0T
+        if self.up0_large:
+            # W[ci][(co, ij)] is used in place; train: W^T [(co, ij)][ci] for the input-gradient GEMM
+            if train:
+                wT = self._buf("up0.WT", (self.KK0 * c0, c0))
+                lb.cdm_transpose(_p(P["up0.0.weight"]), c0, self.KK0 * c0, _p(wT), stream)
+                self.pk["up0.WT"] = wT
+        else:
+            w0 = self._buf("up0.wt", (c0, self.KK0 * c0))
+            w0T = self._buf("up0.wtT", (self.KK0 * c0, c0))
+            lb.cdm_pack_convT(_p(P["up0.0.weight"]), c0, c0, self.KK0, _p(w0), _p(w0T) if train else None, stream)
+            self.pk["up0.wt"], self.pk["up0.wtT"] = w0, w0T
         for m in MLPS:
             w2 = P[m + ".model.2.weight"]
             E = w2.shape[0]
@@ -410,8 +420,11 @@ class UNetEngine:
         ws._mlp = d
         # ---------------- up0: ConvT(k=h/4) on the 1x1 map, GroupNorm(8), ReLU, FiLM1 -> catU1[:, :2nf] ----
         c0 = 2 * nf
-        lb.cdm_gemm_f32(_p(ws.hv), c0, B, c0, _p(self.pk["up0.wt"]), self.KK0 * c0, self.KK0 * c0, _p(ws.y0),
-                        self.KK0 * c0, _p(P["up0.0.bias"]), c0, 0, 1, None, s)
+        if self.up0_large:
+            lb.cdm_up0_fwd(_p(ws.hv), B, c0, _p(P["up0.0.weight"]), self.KK0, _p(P["up0.0.bias"]), _p(ws.y0), s)
+        else:
+            lb.cdm_gemm_f32(_p(ws.hv), c0, B, c0, _p(self.pk["up0.wt"]), self.KK0 * c0, self.KK0 * c0, _p(ws.y0),
+                            self.KK0 * c0, _p(P["up0.0.bias"]), c0, 0, 1, None, s)
         self._gn_fwd(ws, P, "up0.1", Act(ws.y0, c0), B, H2, c0, ws.gn0, stats_from_conv=False, stream=s)
         ce1, te1 = ws.emb["contextembed1"], ws.emb["timeembed1"]
         u1 = ws.catU1.sl(0, c0)
@@ -583,16 +596,28 @@ class UNetEngine:
                      film_out=(ws.d_emb["contextembed1"], ws.d_emb["timeembed1"]))
         # up0 weight: dW[ci][(ij,co)] = sum_n hv[n][ci] dy0[n][(ij,co)]  -> [ci][co][ij]
         KN = self.KK0 * c0
-        sp = lb.raw("cdm_gemm_splits")(B, 1)
-        lb.cdm_gemm_tn_f32(_p(ws.hv), c0, c0, B, _p(ws.D2), KN, KN, 1, _p(ws.slab), s)
-        if sp == 1:   # [ci][ij][co] -> [ci][co][ij]: a batched tiled transpose
-            lb.cdm_transpose_batched(_p(ws.slab), c0, self.KK0, c0, _p(G["up0.0.weight"]), s)
+        if self.up0_large:
+            # dy0 [B][ij][co] -> [B][co][ij]: the K order of W[ci][(co, ij)] (134 MB at config 5, not the weights)
+            lb.cdm_transpose_batched(_p(ws.D2), B, self.KK0, c0, _p(ws.up0T), s)
+            if B <= 16:
+                lb.cdm_up0_wgrad(_p(ws.hv), B, c0, _p(ws.D2), self.KK0, _p(G["up0.0.weight"]), s)
+            else:
+                sp = lb.raw("cdm_gemm_splits")(B, 1)
+                lb.cdm_gemm_tn_f32(_p(ws.hv), c0, c0, B, _p(ws.up0T), KN, KN, 1, _p(ws.slab), s)
+                lb.cdm_slab_reduce(_p(ws.slab), sp, c0, KN, _p(G["up0.0.weight"]), KN, 0, 1, 0, 0, 1.0, s)
+            a_dy, w_t = ws.up0T, self.pk["up0.WT"]
         else:
-            lb.cdm_slab_reduce(_p(ws.slab), sp, c0, KN, _p(G["up0.0.weight"]), KN, 1, self.KK0, c0, 0, 1.0, s)
-        # dhv[n][ci] = sum_{(ij,co)} dy0[n][(ij,co)] W[ci][co][ij]   (split-K over 16*16*2nf)
+            sp = lb.raw("cdm_gemm_splits")(B, 1)
+            lb.cdm_gemm_tn_f32(_p(ws.hv), c0, c0, B, _p(ws.D2), KN, KN, 1, _p(ws.slab), s)
+            if sp == 1:   # [ci][ij][co] -> [ci][co][ij]: a batched tiled transpose
+                lb.cdm_transpose_batched(_p(ws.slab), c0, self.KK0, c0, _p(G["up0.0.weight"]), s)
+            else:
+                lb.cdm_slab_reduce(_p(ws.slab), sp, c0, KN, _p(G["up0.0.weight"]), KN, 1, self.KK0, c0, 0, 1.0, s)
+            a_dy, w_t = ws.D2, self.pk["up0.wtT"]
+        # dhv[n][ci] = sum_k dy0[n][k] W[ci][k] over k = (ij, co) or (co, ij) (large)   (split-K over 16*16*2nf)
         want = max(1, min(64, _cdiv(1024, _cdiv(B, 128) * _cdiv(c0, 128))))
         sp = lb.raw("cdm_gemm_splits")(KN, want)
-        lb.cdm_gemm_f32(_p(ws.D2), KN, B, KN, _p(self.pk["up0.wtT"]), c0, c0, _p(ws.dhv), c0, None, 1, 0, sp,
+        lb.cdm_gemm_f32(_p(a_dy), KN, B, KN, _p(w_t), c0, c0, _p(ws.dhv), c0, None, 1, 0, sp,
                         _p(ws.slab), s)
         if sp > 1:
             lb.cdm_slab_reduce(_p(ws.slab), sp, B, c0, _p(ws.dhv), c0, 0, 1, c0, 0, 1.0, s)
@@ -911,6 +936,7 @@ class Workspace:
             self.dcatU2 = Act(E(P1, 2 * nf), 2 * nf)
             self.dcatU1 = Act(E(P2, 4 * nf), 4 * nf)
             self.dhv = E(B, 2 * nf)
+            self.up0T = E(P2, 2 * nf) if eng.up0_large else None   # dy0 with (co, ij) order (large up0)
             self.coef = [E(C4) for _ in range(3)]
             self.gcoef = [E(B * C4) for _ in range(6)]
             # backward wiring: grad of each layer's output (gout), its dy buffer and dgrad destination
@@ -1001,6 +1027,7 @@ class Workspace:
             need = max(need, wgrad_splits(P0, nf, 9 * 2 * nf) * nf * 9 * 2 * nf)
             for cin, Hin in ((4 * nf, H // 4), (2 * nf, H // 2)):   # convT wgrad
                 need = max(need, wgrad_splits(B * Hin * Hin, cin, 4 * nf) * cin * 4 * nf)
-            need = max(need, 2 * nf * eng.KK0 * 2 * nf)     # up0 weight grad
+            if not (eng.up0_large and B <= 16):             # up0 weight grad through a split-K slab
+                need = max(need, 2 * nf * eng.KK0 * 2 * nf)
             need = max(need, 64 * B * 2 * nf)               # up0 dgrad split-K
         return int(need)

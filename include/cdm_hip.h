@@ -286,6 +286,13 @@ int cdm_transpose(const float* in, int R, int C, float* out, void* stream);
 /* batched: in [batch][R][C] -> out [batch][C][R] (64x64 LDS tiles) */
 int cdm_transpose_batched(const float* in, int batch, int R, int C, float* out, void* stream);
 
+/* up0 on large maps (ContextUnet.py:26-27, ConvTranspose2d(C, C, k, k) on the 1x1 to_vec map, KK = k*k), VALU fp32
+ * kernels over the weights in the reference layout W[ci][co][KK] (no repack): forward y[n][KK][C] (NHWC) =
+ * bias + x[n][:] W (any B >= 1, one read of W per 16 samples); weight gradient dW[ci][co][KK] = x^T dy with
+ * dy [B][KK][C] (NHWC), B <= 16 (assigns).  C % 16 == 0, C <= 512, KK % 64 == 0 (weight gradient: KK % 256 == 0). */
+int cdm_up0_fwd(const float* x, int B, int C, const float* W, int KK, const float* bias, float* y, void* stream);
+int cdm_up0_wgrad(const float* x, int B, int C, const float* dy, int KK, float* dW, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -95,6 +95,7 @@ def _region(live, p):
                                                (64, 2, "h3", 64, True), (16, 1, "x6", 64, True),
                                                (128, 256, "h3", 64, True), (128, 256, "bf16", 64, True),
                                                (128, 1, "h3", 256, True), (256, 16, "h3", 256, True),
+                                               (16, 20, "h3", 256, True),
                                                (128, 512, "h3", 64, False), (256, 32, "h3", 256, False)])
 def test_launch_arguments_stay_in_bounds(monkeypatch, nf, B, math, H, train):
     calls, protos, live = _dry_run(monkeypatch, nf, B, math, H, train)

@@ -518,3 +518,34 @@ def test_batched_repack_equals_per_layer(L, nf):
             assert torch.equal(ta, tb), k
             n += 1
     assert n == 2 * len(shapes)
+
+
+@pytest.mark.parametrize("B,C,k", [(1, 32, 16), (5, 48, 16), (16, 32, 32), (20, 16, 16)])
+def test_up0_large_map_kernels(L, B, C, k):
+    """cdm_up0_fwd / cdm_up0_wgrad (config-5 up0: ConvTranspose2d(C, C, k, k) on the 1x1 to_vec map, weights read in
+    the reference layout) vs torch CPU conv_transpose2d in fp64; fp32 FMA summation -> the fp32 bar of this file.
+    B = 20 > 16: the forward's second 16-sample pass (the weight gradient takes B <= 16 and raises above)."""
+    torch.manual_seed(11)
+    KK = k * k
+    x = torch.randn(B, C, 1, 1, dtype=torch.float64)
+    W = torch.randn(C, C, k, k, dtype=torch.float64) * 0.1
+    b = torch.randn(C, dtype=torch.float64)
+    gy = torch.randn(B, C, k, k, dtype=torch.float64)
+    xg, Wg = x.clone().requires_grad_(), W.clone().requires_grad_()
+    ref = F.conv_transpose2d(xg, Wg, b, stride=k)
+    ref.backward(gy)
+    xc = x.reshape(B, C).float().cuda()
+    Wc, bc = W.float().cuda(), b.float().cuda()
+    y = torch.full((B, KK, C), float("nan"), device="cuda")
+    L.cdm_up0_fwd(xc.data_ptr(), B, C, Wc.data_ptr(), KK, bc.data_ptr(), y.data_ptr(), _s())
+    torch.cuda.synchronize()
+    _close(y.reshape(B, k, k, C).permute(0, 3, 1, 2), ref.detach())
+    gyn = gy.permute(0, 2, 3, 1).reshape(B, KK, C).float().contiguous().cuda()     # NHWC [B][ij][co]
+    dW = torch.full((C, C, k, k), float("nan"), device="cuda")
+    if B > 16:
+        with pytest.raises(Exception):
+            L.cdm_up0_wgrad(xc.data_ptr(), B, C, gyn.data_ptr(), KK, dW.data_ptr(), _s())
+        return
+    L.cdm_up0_wgrad(xc.data_ptr(), B, C, gyn.data_ptr(), KK, dW.data_ptr(), _s())
+    torch.cuda.synchronize()
+    _close(dW, Wg.grad)

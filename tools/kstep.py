@@ -8,6 +8,7 @@ import sys
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 nl = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 idx = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+nl = min(nl, len(idx) - 1)
 steps = [rows[idx[k] + 1: idx[k + 1] + 1] for k in range(len(idx) - 1 - nl, len(idx) - 1)]
 agg = collections.Counter(); cnt = collections.Counter()
 wall = 0.0
