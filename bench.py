@@ -314,11 +314,12 @@ def extra_configs(args, barrier):
     torch.cuda.empty_cache()
     # C5: 256x256 maps, n_feat=256 (1.093 B params; up0 alone 1.07 B), T=2000, split-bf16 fp32-accurate convs
     B5, T5 = args.c5_batch, 2000
-    model, ms, loss = train_rate(256, 256, T5, B5, args.conv_math, 3, 1, 0, barrier)
-    sms, S = sample_rate(model, T5, B5, 0.0, 20, 0, barrier)
+    C5_TRAIN, C5_SAMPLE = 6, 60
+    model, ms, loss = train_rate(256, 256, T5, B5, args.conv_math, C5_TRAIN, 2, 0, barrier)
+    sms, S = sample_rate(model, T5, B5, 0.0, C5_SAMPLE, 0, barrier)
     out["c5_256"] = {"workload": "C5: ContextUnet n_feat=256, 256x256x1, 6 params, T=2000, train-mode BatchNorm",
                      "conv_math": args.conv_math, "batch": B5, "train_img_per_s": round(B5 / (ms * 1e-3), 3),
-                     "train_ms_per_step": round(ms, 3), "train_steps": 3, "final_loss": loss,
+                     "train_ms_per_step": round(ms, 3), "train_steps": C5_TRAIN, "final_loss": loss,
                      "train_tflops": round(3 * 1226.82 * B5 / ms, 2),
                      "sample": {"w=0": {"ms_per_denoise_step": round(sms, 3), "steps_run": S,
                                         "img_per_s": round(B5 / (sms * 1e-3 * T5), 5), "extrapolated_to_T": True}}}
@@ -370,9 +371,9 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--sample-steps", type=int, default=T, help="sampling steps actually run (T=1500 = full)")
     ap.add_argument("--sample-batch", type=int, default=256)
-    ap.add_argument("--cfg-sample-steps", type=int, default=100,
+    ap.add_argument("--cfg-sample-steps", type=int, default=300,
                     help="steps run for the C2 CFG (w=1,3) sampling rates (extrapolated to T)")
-    ap.add_argument("--extra-sample-steps", type=int, default=100, help="sampling steps of the C4 legs")
+    ap.add_argument("--extra-sample-steps", type=int, default=300, help="sampling steps of the C4 legs")
     ap.add_argument("--c5-batch", type=int, default=16)
     ap.add_argument("--no-extra", action="store_true", help="skip the C4 / C5 legs")
     ap.add_argument("--no-cpu", action="store_true")
