@@ -1207,13 +1207,16 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         hb ^= 1;
     }
     unscale<NT>(acc, sx, op_scale<NT>(amax_w));
-    ep(acc, t * HBM_ + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
-    if (nextt) {   // the next tile's chunk 0 (its loads were issued during the last chunk)
-        __syncthreads();                 // the epilogue's scratch aliases the operand LDS
+    if (nextt) {   // the next tile's chunk 0 (its loads were issued during the last chunk) into the halo / B buffers
+        // idle since the last chunk's closing barrier, ahead of the epilogue: its prefetch registers die before the
+        // epilogue and the epilogue needs no barrier pair after it
         store_halo(Hs + hb * NS * HPLANE, 0);
         store_b(bb * BPL * XPLANE, bregA);
-        __syncthreads();
     }
+    // epilogue scratch (stats / max-min: 4 KiB): the other halo buffer (>= 24 KiB), last read by the final chunk
+    // before its closing barrier
+    ep(acc, t * HBM_ + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(Hs + (hb ^ 1) * NS * HPLANE), tid);
+    if (nextt) __syncthreads();
     }
 }
 
