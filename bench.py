@@ -44,6 +44,15 @@ CONV_MATH_INFO = {"fp32": (0, "fp32 MFMA v_mfma_f32_32x32x2_f32"),
 NT_CODE = {"fp32": 0, "x6": 6, "h3": 4}   # engine / C-ABI arithmetic code
 
 
+_T0 = time.perf_counter()
+
+
+def _progress(msg: str):
+    """One progress line per leg / CPU step on stderr (the run writes its JSON only at the end; a long silent run
+    reads as hung to the GPU harness)."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def _dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -177,6 +186,7 @@ def _cpu_train_rate(R, nf: int, T: int, bs: int, steps: int, warmup: int):
         noise = torch.randn(bs, 1, H, H, generator=g)
         t = torch.randint(1, T + 1, (bs,), generator=g)
         tr.step(x, c, noise, t, T, ab, lambda: R.draw_shortcut(1, nf))
+        _progress(f"cpu train step n_feat={nf} bs={bs}")
 
     for _ in range(warmup):
         one()
@@ -205,6 +215,8 @@ def _cpu_sample_rate(R, sd, nf: int, T: int, n: int, w: float, steps: int):
         else:
             eps = fn(x, t, params)
         x = R.denoise_add_noise(x, i, eps, z, b, a, ab)
+        if n > 8:
+            _progress(f"cpu sample step n={n} w={w:g}")
     return (time.perf_counter() - t0) / steps
 
 
@@ -300,12 +312,14 @@ def extra_configs(args, barrier):
     out = {}
     # C4: bf16 MFMA operands, fp32 accumulate / master weights / activations; CFG w in {0,1,3}
     model, ms, loss = train_rate(NF, H, T, args.batch, "bf16", 10, 3, 0, barrier)
+    _progress(f"C4 train {ms:.3f} ms/step")
     c4 = {"workload": "C4: ContextUnet n_feat=128 64x64, bf16 mixed-precision convs (bf16 operands, fp32 "
                       "accumulate, fp32 master weights / activations / norms), T=1500",
           "batch": args.batch, "train_img_per_s": round(args.batch / (ms * 1e-3), 2), "train_ms_per_step": round(ms, 3),
           "train_steps": 10, "final_loss": loss, "sample": {}}
     for w in (0.0, 1.0, 3.0):
         sms, S = sample_rate(model, T, args.sample_batch, w, args.extra_sample_steps, 0, barrier)
+        _progress(f"C4 sample w={w:g} {sms:.3f} ms/step")
         c4["sample"][f"w={w:g}"] = {"ms_per_denoise_step": round(sms, 3), "steps_run": S,
                                    "img_per_s": round(args.sample_batch / (sms * 1e-3 * T), 4),
                                    "extrapolated_to_T": S < T}
@@ -316,7 +330,9 @@ def extra_configs(args, barrier):
     B5, T5 = args.c5_batch, 2000
     C5_TRAIN, C5_SAMPLE = 6, 60
     model, ms, loss = train_rate(256, 256, T5, B5, args.conv_math, C5_TRAIN, 2, 0, barrier)
+    _progress(f"C5 train {ms:.3f} ms/step")
     sms, S = sample_rate(model, T5, B5, 0.0, C5_SAMPLE, 0, barrier)
+    _progress(f"C5 sample {sms:.3f} ms/step")
     out["c5_256"] = {"workload": "C5: ContextUnet n_feat=256, 256x256x1, 6 params, T=2000, train-mode BatchNorm",
                      "conv_math": args.conv_math, "batch": B5, "train_img_per_s": round(B5 / (ms * 1e-3), 3),
                      "train_ms_per_step": round(ms, 3), "train_steps": C5_TRAIN, "final_loss": loss,
@@ -409,14 +425,17 @@ def main():
                                                          barrier, use_graph=not args.no_graph, dist=dist,
                                                          conv_probe=True)
     train_ips = world * B / (ms_step * 1e-3)
+    _progress(f"C2 train {ms_step:.3f} ms/step")
 
     # ---------------- sampling (replicas) ----------------
     n = args.sample_batch
     sms, S = sample_rate(model, T, n, 0.0, args.sample_steps, rank, barrier, dist)
     sample_ips = world * n / (sms * 1e-3 * T)
+    _progress(f"C2 sample w=0 {sms:.3f} ms/step")
     cfg = {}
     for w in (1.0, 3.0):
         cms, CS = sample_rate(model, T, n, w, args.cfg_sample_steps, rank, barrier, dist)
+        _progress(f"C2 sample w={w:g} {cms:.3f} ms/step")
         cfg[f"w={w:g}"] = {"ms_per_denoise_step": round(cms, 3), "steps_run": CS,
                            "img_per_s": round(world * n / (cms * 1e-3 * T), 4), "extrapolated_to_T": CS < T}
     del model
