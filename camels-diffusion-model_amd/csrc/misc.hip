@@ -122,9 +122,15 @@ __global__ __launch_bounds__(256) void conv_cin1_fwd_kernel(const float* x, int 
     }
 }
 
+// BN backward of the init conv's Conv -> BatchNorm -> ReLU applied while reading its dy (FUSED): dy is never written
+struct Cin1BnBwd { const float* y; int ldy; const float* p[7]; };   // s, t, mean, invstd, A, B, Cc
+
 // per-(n, chunk) partials R = 10: r<9 -> sum dy[p][c]*x[p+tap_r], r=9 -> sum dy[p][c]
+// FUSED: dy = bn_bwd_elem(g, y) from the grad g of the ReLU output and the pre-norm y (the expression of
+// norm_apply_bwd_kernel: bit-identical dy, no 537 MB write + read of it at bs=256)
+template <bool FUSED>
 __global__ __launch_bounds__(256) void conv_cin1_wgrad_kernel(const float* dy, int lddy, const float* x, int H, int W,
-                                                              int C, int csize, float* slab) {
+                                                              int C, int csize, float* slab, Cin1BnBwd bn) {
     constexpr int R = 10;
     __shared__ float red[256 * 4 * R];
     const int C4 = C >> 2, P = 256 / C4, tid = threadIdx.x, c4 = (tid % C4) * 4, pl = tid / C4;
@@ -138,7 +144,16 @@ __global__ __launch_bounds__(256) void conv_cin1_wgrad_kernel(const float* dy, i
     if (pl < P) {
         for (int p = p0 + pl; p < p1; p += P) {
             const int h = p / W, w = p - h * W;
-            const float4 g = ld4(dy + ((long long)n * HW + p) * lddy + c4);
+            float4 g = ld4(dy + ((long long)n * HW + p) * lddy + c4);
+            if constexpr (FUSED) {
+                const float4 yv = ld4(bn.y + ((long long)n * HW + p) * bn.ldy + c4);
+                float gv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    gv[j] = bn_bwd_elem(gv[j], f4get(yv, j), bn.p[0][c4 + j], bn.p[1][c4 + j], bn.p[2][c4 + j],
+                                        bn.p[3][c4 + j], bn.p[4][c4 + j], bn.p[5][c4 + j], bn.p[6][c4 + j]);
+                g = make_float4(gv[0], gv[1], gv[2], gv[3]);
+            }
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
                 const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
@@ -786,8 +801,20 @@ CDM_API int cdm_conv3x3_cin1_fwd(const float* x, int N, int H, int W, const floa
 CDM_API int cdm_conv3x3_cin1_wgrad(const float* dy, int lddy, const float* x, int N, int H, int W, int C, int csize,
                                    float* slab, void* stream) {
     if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(conv_cin1_wgrad_kernel, dim3((H * W + csize - 1) / csize, N), dim3(256), 0, S(stream), dy, lddy, x,
-                       H, W, C, csize, slab);
+    hipLaunchKernelGGL(conv_cin1_wgrad_kernel<false>, dim3((H * W + csize - 1) / csize, N), dim3(256), 0, S(stream), dy,
+                       lddy, x, H, W, C, csize, slab, Cin1BnBwd{});
+    return cdm_status();
+}
+// cdm_conv3x3_cin1_wgrad of a Conv -> BatchNorm -> ReLU layer with its BN backward applied while reading dy: g = grad of
+// the ReLU output, y = pre-norm activations, s / t / mean / invstd / A / B / Cc per channel (as cdm_norm_apply_bwd mode 0)
+CDM_API int cdm_conv3x3_cin1_wgrad_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
+                                         const float* t, const float* mean, const float* invstd, const float* A,
+                                         const float* B, const float* Cc, const float* x, int N, int H, int W, int C,
+                                         int csize, float* slab, void* stream) {
+    if (C % 4 || C > 1024 || ldg % 4 || ldy % 4) return (int)hipErrorInvalidValue;
+    const Cin1BnBwd bn{y, ldy, {s, t, mean, invstd, A, B, Cc}};
+    hipLaunchKernelGGL(conv_cin1_wgrad_kernel<true>, dim3((H * W + csize - 1) / csize, N), dim3(256), 0, S(stream), g,
+                       ldg, x, H, W, C, csize, slab, bn);
     return cdm_status();
 }
 CDM_API int cdm_slab_sum_all(const double* part, int nparts, int R, int r0, int rn, int C, float* out, long long s_r,

@@ -120,6 +120,8 @@ class UNetEngine:
         self.fuse_bn_bwd = self.nterm == NT_H3 and os.environ.get("CDM_FUSE_BN_BWD", "1") != "0"
         # h3 train: a dense BatchNorm + ReLU applied inside the next conv's staging ($CDM_FUSE_BN_FWD=0: apply kernel)
         self.fuse_bn_fwd = self.nterm == NT_H3 and os.environ.get("CDM_FUSE_BN_FWD", "1") != "0"
+        # init_conv.conv1's BN backward inside its weight-gradient kernel ($CDM_FUSE_CIN1_BWD=0: the apply kernel)
+        self.fuse_cin1_bwd = os.environ.get("CDM_FUSE_CIN1_BWD", "1") != "0"
         self.device = torch.device(device)
         self.layers = conv_layers(n_feat, height)
         self.L = {l.name: l for l in self.layers}
@@ -691,6 +693,15 @@ class UNetEngine:
             lb.cdm_conv3x3_dgrad_h3_bnbwd(g.p, g.ld, _p(y), C, *coef, B, S, S, C, _p(self.pk[key + "_x"]), dslot,
                                           _p(self.pk[key + "_amax"]), dgd.p, dgd.ld, l.cin,
                                           EPI_ACCUM if ws.dgrad_accum[l.name] else 0, gslot, s)
+            return
+        if l.cin == 1 and mode == 0 and self.fuse_cin1_bwd:
+            # init_conv.conv1: only a weight gradient (the input needs none); its BN backward runs while that kernel
+            # reads g and y (bit-identical dy, never written)
+            lb.cdm_conv3x3_cin1_wgrad_bnbwd(g.p, g.ld, _p(y), C, _p(st["scale"]), _p(st["shift"]), _p(st["mean"]),
+                                            _p(st["invstd"]), _p(co[0]), _p(co[1]), _p(co[2]), _p(ws.x_in), B, S, S,
+                                            C, CHUNK, _p(ws.slab), s)
+            nparts = fold(ws, _p(ws.slab), B * _cdiv(S * S, CHUNK), 10, C, s)
+            lb.cdm_slab_sum_all(_p(ws.dpart), nparts, 10, 0, 9, C, _p(G[l.w]), 1, 9, 0, s)
             return
         dy = ws.dy[l.name]
         dslot = self._slot(ws, "dy:" + l.name) if l.cin > 1 else None

@@ -218,6 +218,13 @@ int cdm_conv3x3_cin1_fwd(const float* x, int N, int H, int W, const float* wt, c
                          int C, int relu, void* stream);
 int cdm_conv3x3_cin1_wgrad(const float* dy, int lddy, const float* x, int N, int H, int W, int C, int csize,
                            float* slab, void* stream);
+/* cdm_conv3x3_cin1_wgrad of the init conv's Conv -> BatchNorm -> ReLU with its BN backward applied while reading: g =
+ * grad of the ReLU output, y = pre-norm activations, per-channel s, t, mean, invstd, A, B, Cc as cdm_norm_apply_bwd
+ * mode 0 (bit-identical dy, never written).  Replaces the autograd BatchNorm2d backward + Conv2d weight grad of
+ * ContextUnet.py:14 (init_conv.conv1, diffusion_utilities.py:26-30). */
+int cdm_conv3x3_cin1_wgrad_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
+                                 const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
+                                 const float* x, int N, int H, int W, int C, int csize, float* slab, void* stream);
 int cdm_slab_sum_all(const double* part, int nparts, int R, int r0, int rn, int C, float* out, long long s_r,
                      long long s_c, int accumulate, void* stream);
 /* out.3: Conv2d(nf, 1, 3, 1, 1) (ContextUnet.py:39) */

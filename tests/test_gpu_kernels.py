@@ -549,3 +549,26 @@ def test_up0_large_map_kernels(L, B, C, k):
     L.cdm_up0_wgrad(xc.data_ptr(), B, C, gyn.data_ptr(), KK, dW.data_ptr(), _s())
     torch.cuda.synchronize()
     _close(dW, Wg.grad)
+
+
+def test_cin1_wgrad_bn_backward_fused_bit_exact(L):
+    """init_conv.conv1's weight gradient with its BatchNorm backward applied while reading g and y
+    (cdm_conv3x3_cin1_wgrad_bnbwd) == the apply kernel (cdm_norm_apply_bwd mode 0) followed by
+    cdm_conv3x3_cin1_wgrad, partial for partial (the same bn_bwd_elem expression, the same summation order)."""
+    N, H, C = 3, 64, 128
+    P = N * H * H
+    g_ = torch.Generator(device="cuda").manual_seed(31)
+    r = lambda *s: torch.randn(*s, device="cuda", generator=g_)   # noqa: E731
+    gin, y, x = r(P, C), r(P, C), r(N, H, H)
+    co = [r(C), r(C) * 0.1, r(C) * 0.2, r(C).abs() + 0.5, r(C), r(C) * 1e-3, r(C) * 1e-3]   # s t mean invstd A B Cc
+    nch = (H * H + 127) // 128
+    ref, got = (torch.full((N * nch * 10 * C,), float("nan"), device="cuda") for _ in range(2))
+    dy = torch.empty(P, C, device="cuda")
+    L.cdm_norm_apply_bwd(0, gin.data_ptr(), C, y.data_ptr(), C, N, H, H, C, co[0].data_ptr(), co[1].data_ptr(), 0,
+                         co[2].data_ptr(), co[3].data_ptr(), 0, 1, None, 0, co[4].data_ptr(), co[5].data_ptr(),
+                         co[6].data_ptr(), 0, dy.data_ptr(), C, None, _s())
+    L.cdm_conv3x3_cin1_wgrad(dy.data_ptr(), C, x.data_ptr(), N, H, H, C, 128, ref.data_ptr(), _s())
+    L.cdm_conv3x3_cin1_wgrad_bnbwd(gin.data_ptr(), C, y.data_ptr(), C, *[t.data_ptr() for t in co], x.data_ptr(), N, H,
+                                   H, C, 128, got.data_ptr(), _s())
+    torch.cuda.synchronize()
+    assert torch.isfinite(ref).all() and torch.equal(got, ref)
