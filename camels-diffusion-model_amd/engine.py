@@ -323,15 +323,19 @@ class UNetEngine:
         """Producer l's train-mode BatchNorm apply (z = relu(y s + t)) runs inside the staging of the next conv (its
         forward and its weight gradient): z is never written.  Needs the LDS-halo path for both convs (max / min
         epilogue on l, BN-ReLU staging on the consumer) and the kernel-row weight gradient for the consumer."""
-        if not (self.fuse_bn_fwd and kind == "dense" and l.cin > 1 and self.halo_addressable(B, l.S)):
+        if not (self.fuse_bn_fwd and kind == "dense" and self.halo_addressable(B, l.S)):
+            return False
+        if l.cin == 1 and os.environ.get("CDM_FUSE_CIN1_FWD", "1") == "0":   # A/B switch of the init conv's fusion
             return False
         i = self.layers.index(l)
         if i + 1 >= len(self.layers):
             return False
         c = self.layers[i + 1]
         halo = lambda L: L.kc == 16 and L.S in (32, 64, 128, 256) and (L.S * L.S) % 256 == 0   # noqa: E731
-        return (halo(l) and halo(c) and c.cin == l.cout and c.cin <= 256 and c.cin % 128 == 0 and c.cout % 128 == 0
-                and c.S == l.S)
+        # the producer's max / min of y: from its conv epilogue (LDS-halo path), or from the statistics pass of the
+        # C_in = 1 init conv (cdm_reduce_stats_mm)
+        return ((l.cin == 1 or halo(l)) and halo(c) and c.cin == l.cout and c.cin <= 256 and c.cin % 128 == 0
+                and c.cout % 128 == 0 and c.S == l.S)
 
     def fuses_bn_bwd(self, l: "LayerSpec", kind: str, B: int = 1) -> bool:
         """Layer l's BN backward runs inside its dgrad / wgrad staging (cdm_conv3x3_*_h3_bnbwd)."""
@@ -472,7 +476,8 @@ class UNetEngine:
             if l.cin == 1:
                 lb.cdm_conv3x3_cin1_fwd(_p(x), B, S, S, _p(self.pk[l.name + ".wpk"]), _p(P[l.b]), _p(y), l.cout,
                                         l.cout, 0, s)
-                lb.cdm_reduce_stats(_p(y), l.cout, B, S * S, l.cout, CHUNK, _p(ws.slab), s)
+                ymm_p, ymm_ld = ws.ymm_of(l) if l.name in ws.fused_fwd else (None, 0)
+                lb.cdm_reduce_stats_mm(_p(y), l.cout, B, S * S, l.cout, CHUNK, _p(ws.slab), ymm_p, ymm_ld, s)
                 ntiles = B * _cdiv(S * S, CHUNK)
             else:
                 yslot = self._slot(ws, "y:" + l.name) if l.name in ws.fused else None

@@ -165,6 +165,11 @@ int cdm_slab_reduce(const float* slab, int splits, int M, int N, float* out, lon
 /* ---- normalisation / pooling / FiLM (csrc/norm.hip) ------------------------------------------- */
 /* per-(image, pixel-chunk) partial sums (slab[N][chunks][R][C]) */
 int cdm_reduce_stats(const float* y, int ldy, int N, int HW, int C, int csize, float* slab, void* stream);
+/* cdm_reduce_stats (identical slab) + optional (ymm != NULL) per-channel max / min of y as ordered-int keys, atomic max
+ * into ymm[c] / min into ymm[ymm_ld + c] (cleared by the caller to INT_MIN / INT_MAX): the C_in = 1 init conv's
+ * BatchNorm statistics when its BN-ReLU apply runs in the next conv's staging. */
+int cdm_reduce_stats_mm(const float* y, int ldy, int N, int HW, int C, int csize, float* slab, int* ymm, int ymm_ld,
+                        void* stream);
 int cdm_reduce_sum(const float* g, int ldg, int N, int HW, int C, int csize, float* slab, void* stream);
 /* BatchNorm2d / GroupNorm(8) + ReLU (+MaxPool2d(2) | +FiLM) backward sums (mode 0 plain, 1 pool, 2 FiLM) */
 int cdm_norm_bwd_reduce(int mode, const float* g, int ldg, const float* y, int ldy, int N, int H, int W, int C,

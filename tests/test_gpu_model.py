@@ -257,7 +257,8 @@ def test_eval_forward_under_grad_mode():
 
 @pytest.mark.parametrize("B", [2, 5])
 def test_fused_bn_fwd_bit_exact_nf128(B):
-    """h3 train at n_feat=128: the 12 dense BatchNorm + ReLU applies fused into the next conv's staging (forward and
+    """h3 train at n_feat=128: the 13 dense BatchNorm + ReLU applies (incl. the C_in = 1 init conv's, whose max / min
+    come from its statistics pass) fused into the next conv's staging (forward and
     weight gradient; z never written; its h3 scale from the producer's per-channel max / min) == the separate apply
     kernel ($CDM_FUSE_BN_FWD=0), bit for bit: output, every gradient, BatchNorm running statistics."""
     nf, T = 128, 1500
@@ -278,7 +279,7 @@ def test_fused_bn_fwd_bit_exact_nf128(B):
             pred = m(xp.cuda(), (tt / T).cuda(), c.cuda())
             F.mse_loss(pred, noise.cuda()).backward()
             ws = eng.workspace(B, True)
-            assert len(ws.fused_fwd) == (12 if fuse else 0)
+            assert len(ws.fused_fwd) == (13 if fuse else 0)
             res.append((pred.detach().cpu(), {k: p.grad.detach().cpu() for k, p in m.named_parameters()},
                         {k: v.detach().cpu() for k, v in m.state_dict().items() if "running" in k}))
     finally:
