@@ -90,20 +90,23 @@ __global__ void philox_randint_kernel(int* out, int n, int lo, int hi, unsigned 
 // conv3x3, C_in = 1:  y[p][co] = b[co] + sum_tap x[p+tap] * wt[tap][co]   (wt = pack_conv3x3 output, Cin = 1)
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void conv_cin1_fwd_kernel(const float* x, int N, int H, int W, const float* w9,
-                                                            const float* bias, float* y, int ldy, int C, int relu) {
+                                                            const float* bias, float* y, int ldy, int C, int relu,
+                                                            float* amax) {
     // lanes span channels (one float4 each; a pixel's C channels are one coalesced row), the 9 input
     // taps are wave-uniform broadcast loads, the 9x4 weights of a lane stay in registers.
+    // amax (optional): running max|y| for the consuming h3 conv's operand scale (block_amax_commit)
     const int C4 = C >> 2, PP = 256 / C4;
     const int c4 = (threadIdx.x % C4) * 4, pl = threadIdx.x / C4;
-    if (pl >= PP) return;
+    float am = 0.f;
+    const bool active = pl < PP;      // (every thread reaches the block max at the end: it synchronises the block)
     float wr[9][4], bb[4];
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wr[tap][j] = w9[tap * C + c4 + j];
+        for (int j = 0; j < 4; ++j) wr[tap][j] = active ? w9[tap * C + c4 + j] : 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bb[j] = bias[c4 + j];
-    const long long P = (long long)N * H * W;
+    for (int j = 0; j < 4; ++j) bb[j] = active ? bias[c4 + j] : 0.f;
+    const long long P = active ? (long long)N * H * W : 0;
     for (long long pix = (long long)blockIdx.x * PP + pl; pix < P; pix += (long long)gridDim.x * PP) {
         const int n = (int)(pix / (H * W)), rem = (int)(pix - (long long)n * H * W), h = rem / W, w = rem - h * W;
         float o[4] = {bb[0], bb[1], bb[2], bb[3]};
@@ -118,8 +121,11 @@ __global__ __launch_bounds__(256) void conv_cin1_fwd_kernel(const float* x, int 
 #pragma unroll
             for (int j = 0; j < 4; ++j) o[j] = relu_f(o[j]);
         }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) am = fmaxf(am, fabsf(o[j]));
         st4(y + pix * ldy + c4, make_float4(o[0], o[1], o[2], o[3]));
     }
+    if (amax) block_amax_commit(am, amax);
 }
 
 // BN backward of the init conv's Conv -> BatchNorm -> ReLU applied while reading its dy (FUSED): dy is never written
@@ -790,12 +796,12 @@ CDM_API int cdm_philox_randint(int* out, int n, int lo, int hi, unsigned long lo
     return cdm_status();
 }
 CDM_API int cdm_conv3x3_cin1_fwd(const float* x, int N, int H, int W, const float* w9, const float* bias, float* y,
-                                 int ldy, int C, int relu, void* stream) {
+                                 int ldy, int C, int relu, float* amax, void* stream) {
     if (C % 4) return (int)hipErrorInvalidValue;
     if (C > 1024) return (int)hipErrorInvalidValue;
     const long long P = (long long)N * H * W;
     hipLaunchKernelGGL(conv_cin1_fwd_kernel, dim3(nblocks(P, 256 / (C / 4), 4096)), dim3(256), 0, S(stream), x, N, H, W, w9,
-                       bias, y, ldy, C, relu);
+                       bias, y, ldy, C, relu, amax);
     return cdm_status();
 }
 CDM_API int cdm_conv3x3_cin1_wgrad(const float* dy, int lddy, const float* x, int N, int H, int W, int C, int csize,

@@ -475,7 +475,7 @@ class UNetEngine:
         if ws.train:
             if l.cin == 1:
                 lb.cdm_conv3x3_cin1_fwd(_p(x), B, S, S, _p(self.pk[l.name + ".wpk"]), _p(P[l.b]), _p(y), l.cout,
-                                        l.cout, 0, s)
+                                        l.cout, 0, None, s)
                 ymm_p, ymm_ld = ws.ymm_of(l) if l.name in ws.fused_fwd else (None, 0)
                 lb.cdm_reduce_stats_mm(_p(y), l.cout, B, S * S, l.cout, CHUNK, _p(ws.slab), ymm_p, ymm_ld, s)
                 ntiles = B * _cdiv(S * S, CHUNK)
@@ -506,9 +506,7 @@ class UNetEngine:
             dslot = self._dst_slot(ws, l) if dense else None
             if l.cin == 1:
                 lb.cdm_conv3x3_cin1_fwd(_p(x), B, S, S, _p(self.pk[l.name + ".wpk_e"]),
-                                        _p(self.pk[l.name + ".bpk_e"]), outp.p, outp.ld, l.cout, 1, s)
-                if dslot is not None:   # the direct C_in = 1 conv has no fused max: one pass over its output
-                    lb.cdm_amax_f32(outp.p, B * S * S, l.cout, outp.ld, dslot, 1, s)
+                                        _p(self.pk[l.name + ".bpk_e"]), outp.p, outp.ld, l.cout, 1, dslot, s)
             else:
                 self.conv3x3(l.name + ".wpk_e", src.p, B, S, l.cin, src.ld, _p(self.pk[l.name + ".bpk_e"]), outp.p,
                              outp.ld, l.cout, EPI_RELU, None, 0, l.kc, s, amax_x=self._src_slot(ws, l),

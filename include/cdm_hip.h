@@ -220,7 +220,7 @@ int cdm_bn_bwd_amax_bound(int C, const float* A, const float* B, const float* Cc
 /* ---- small ops (csrc/misc.hip) ---------------------------------------------------------------- */
 /* init_conv.conv1: Conv2d(1, nf, 3, 1, 1) (ContextUnet.py:14 -> diffusion_utilities.py:27) */
 int cdm_conv3x3_cin1_fwd(const float* x, int N, int H, int W, const float* wt, const float* bias, float* y, int ldy,
-                         int C, int relu, void* stream);
+                         int C, int relu, float* amax, void* stream);   /* amax: optional running max|y| (atomic) */
 int cdm_conv3x3_cin1_wgrad(const float* dy, int lddy, const float* x, int N, int H, int W, int C, int csize,
                            float* slab, void* stream);
 /* cdm_conv3x3_cin1_wgrad of the init conv's Conv -> BatchNorm -> ReLU with its BN backward applied while reading: g =
