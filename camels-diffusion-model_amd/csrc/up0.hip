@@ -105,6 +105,56 @@ __global__ __launch_bounds__(256) void up0_wgrad_kernel(const float* __restrict_
     }
 }
 
+// input gradient: dx[n][ci] = sum_k dyT[n][k] W[ci][k], k = (co, ij) (dyT = dy transposed per sample to [n][co][ij]).
+// Block: 64 ci x one K range of KR; thread = (ci group of 8: tid >> 5, k lane: tid & 31) owns acc[8 ci][16 n] over the
+// k = k0 + 4 lane + 128 s of its range: per k step 8 float4 of W (each 32-lane half-wave reads 512 contiguous bytes of
+// one W row) and the 16 n rows of dyT at the same k (shared by the 8 ci groups through L1), 512 FMAs.  W is read
+// exactly once; the 32 k lanes fold through shuffles at the end; per-split partials slab[split][n < B][ci].
+constexpr int U0D_KR = 32768;
+__global__ __launch_bounds__(256, 2) void up0_dgrad_kernel(const float* __restrict__ dyT, int B, int C,
+                                                           const float* __restrict__ W, long long K,
+                                                           float* __restrict__ slab) {
+    const int tid = threadIdx.x, kl = tid & 31, cg = tid >> 5;
+    const int ci0 = blockIdx.x * 64 + cg * 8;
+    const long long k0 = (long long)blockIdx.y * U0D_KR, k1 = min(K, k0 + U0D_KR);
+    float acc[8][U0_NB];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int n = 0; n < U0_NB; ++n) acc[c][n] = 0.f;
+    for (long long k = k0 + kl * 4; k < k1; k += 128) {
+        float4 w[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) w[c] = ld4(W + (long long)(ci0 + c) * K + k);
+#pragma unroll
+        for (int n = 0; n < U0_NB; ++n) {
+            const float4 d = n < B ? ld4(dyT + (long long)n * K + k) : f4zero();
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                acc[c][n] = fmaf(d.w, w[c].w, fmaf(d.z, w[c].z, fmaf(d.y, w[c].y, fmaf(d.x, w[c].x, acc[c][n]))));
+        }
+    }
+    // fold the 32 k lanes (lanes 0-31 and 32-63 of a wave are different ci groups)
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int n = 0; n < U0_NB; ++n) {
+            float v = acc[c][n];
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+            acc[c][n] = v;
+        }
+    if (kl == 0) {
+        float* out = slab + (long long)blockIdx.y * B * C;
+#pragma unroll
+        for (int n = 0; n < U0_NB; ++n) {
+            if (n >= B) break;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) out[n * C + ci0 + c] = acc[c][n];
+        }
+    }
+}
+
 static bool u0_shape_ok(int C, int KK) { return C % 16 == 0 && C <= U0_CMAX && KK % 64 == 0; }
 static bool u0_wgrad_shape_ok(int C, int KK) { return C % 16 == 0 && C <= U0_CMAX && KK % 256 == 0; }
 
@@ -115,6 +165,16 @@ CDM_API int cdm_up0_fwd(const float* x, int B, int C, const float* W, int KK, co
                        y);
     return cdm_status();
 }
+
+// slab [ceil(C*KK / 32768)][B][C] of per-K-range partials; cdm_slab_reduce folds them
+CDM_API int cdm_up0_dgrad(const float* dyT, int B, int C, const float* W, int KK, float* slab, void* stream) {
+    if (B < 1 || B > U0_NB || C % 64 || C > U0_CMAX || KK % 64) return (int)hipErrorInvalidValue;
+    const long long K = (long long)C * KK;
+    hipLaunchKernelGGL(up0_dgrad_kernel, dim3(C / 64, (unsigned)((K + U0D_KR - 1) / U0D_KR)), dim3(256), 0,
+                       (hipStream_t)stream, dyT, B, C, W, K, slab);
+    return cdm_status();
+}
+CDM_API int cdm_up0_dgrad_splits(int C, int KK) { return (int)(((long long)C * KK + U0D_KR - 1) / U0D_KR); }
 
 CDM_API int cdm_up0_wgrad(const float* x, int B, int C, const float* dy, int KK, float* dW, void* stream) {
     if (B < 1 || B > U0_NB || !u0_wgrad_shape_ok(C, KK)) return (int)hipErrorInvalidValue;

@@ -230,11 +230,7 @@ class UNetEngine:
                     self._split(name + ".wtT", 4 * nf, cin, stream)
         c0 = 2 * nf
         if self.up0_large:
-            # W[ci][(co, ij)] is used in place; train: W^T [(co, ij)][ci] for the input-gradient GEMM
-            if train:
-                wT = self._buf("up0.WT", (self.KK0 * c0, c0))
-                lb.cdm_transpose(_p(P["up0.0.weight"]), c0, self.KK0 * c0, _p(wT), stream)
-                self.pk["up0.WT"] = wT
+            pass   # W[ci][(co, ij)] is used in place (B > 16 input gradients build their W^T in the backward)
         else:
             w0 = self._buf("up0.wt", (c0, self.KK0 * c0))
             w0T = self._buf("up0.wtT", (self.KK0 * c0, c0))
@@ -604,13 +600,20 @@ class UNetEngine:
         if self.up0_large:
             # dy0 [B][ij][co] -> [B][co][ij]: the K order of W[ci][(co, ij)] (134 MB at config 5, not the weights)
             lb.cdm_transpose_batched(_p(ws.D2), B, self.KK0, c0, _p(ws.up0T), s)
-            if B <= 16:
+            if B <= 16 and c0 % 64 == 0:
                 lb.cdm_up0_wgrad(_p(ws.hv), B, c0, _p(ws.D2), self.KK0, _p(G["up0.0.weight"]), s)
+                # input gradient over W in place (VALU, W read once): per-K-range partials folded over the splits
+                sp = lb.raw("cdm_up0_dgrad_splits")(c0, self.KK0)
+                lb.cdm_up0_dgrad(_p(ws.up0T), B, c0, _p(P["up0.0.weight"]), self.KK0, _p(ws.slab), s)
+                lb.cdm_slab_reduce(_p(ws.slab), sp, B, c0, _p(ws.dhv), c0, 0, 1, c0, 0, 1.0, s)
+                a_dy = None
             else:
                 sp = lb.raw("cdm_gemm_splits")(B, 1)
                 lb.cdm_gemm_tn_f32(_p(ws.hv), c0, c0, B, _p(ws.up0T), KN, KN, 1, _p(ws.slab), s)
                 lb.cdm_slab_reduce(_p(ws.slab), sp, c0, KN, _p(G["up0.0.weight"]), KN, 0, 1, 0, 0, 1.0, s)
-            a_dy, w_t = ws.up0T, self.pk["up0.WT"]
+                wT = self.pk["up0.WT"] = self._buf("up0.WT", (KN, c0))
+                lb.cdm_transpose(_p(P["up0.0.weight"]), c0, KN, _p(wT), s)
+                a_dy, w_t = ws.up0T, wT
         else:
             sp = lb.raw("cdm_gemm_splits")(B, 1)
             lb.cdm_gemm_tn_f32(_p(ws.hv), c0, c0, B, _p(ws.D2), KN, KN, 1, _p(ws.slab), s)
@@ -620,12 +623,13 @@ class UNetEngine:
                 lb.cdm_slab_reduce(_p(ws.slab), sp, c0, KN, _p(G["up0.0.weight"]), KN, 1, self.KK0, c0, 0, 1.0, s)
             a_dy, w_t = ws.D2, self.pk["up0.wtT"]
         # dhv[n][ci] = sum_k dy0[n][k] W[ci][k] over k = (ij, co) or (co, ij) (large)   (split-K over 16*16*2nf)
-        want = max(1, min(64, _cdiv(1024, _cdiv(B, 128) * _cdiv(c0, 128))))
-        sp = lb.raw("cdm_gemm_splits")(KN, want)
-        lb.cdm_gemm_f32(_p(a_dy), KN, B, KN, _p(w_t), c0, c0, _p(ws.dhv), c0, None, 1, 0, sp,
-                        _p(ws.slab), s)
-        if sp > 1:
-            lb.cdm_slab_reduce(_p(ws.slab), sp, B, c0, _p(ws.dhv), c0, 0, 1, c0, 0, 1.0, s)
+        if a_dy is not None:
+            want = max(1, min(64, _cdiv(1024, _cdiv(B, 128) * _cdiv(c0, 128))))
+            sp = lb.raw("cdm_gemm_splits")(KN, want)
+            lb.cdm_gemm_f32(_p(a_dy), KN, B, KN, _p(w_t), c0, c0, _p(ws.dhv), c0, None, 1, 0, sp,
+                            _p(ws.slab), s)
+            if sp > 1:
+                lb.cdm_slab_reduce(_p(ws.slab), sp, B, c0, _p(ws.dhv), c0, 0, 1, c0, 0, 1.0, s)
         # to_vec: d2 grad += dhv * gelu'(hpre) / (h/4)^2
         d2g = ws.dcatU1.sl(2 * nf, 2 * nf)
         lb.cdm_avgpool_gelu_bwd(_p(ws.dhv), _p(ws.hpre), B, H2 * H2, c0, d2g.p, d2g.ld, s)
@@ -1044,4 +1048,6 @@ class Workspace:
             if not (eng.up0_large and B <= 16):             # up0 weight grad through a split-K slab
                 need = max(need, 2 * nf * eng.KK0 * 2 * nf)
             need = max(need, 64 * B * 2 * nf)               # up0 dgrad split-K
+            if eng.up0_large:                               # cdm_up0_dgrad partials (32768-wide K ranges)
+                need = max(need, _cdiv(2 * nf * eng.KK0, 32768) * B * 2 * nf)
         return int(need)

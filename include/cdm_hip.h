@@ -304,6 +304,10 @@ int cdm_transpose_batched(const float* in, int batch, int R, int C, float* out, 
  * dy [B][KK][C] (NHWC), B <= 16 (assigns).  C % 16 == 0, C <= 512, KK % 64 == 0 (weight gradient: KK % 256 == 0). */
 int cdm_up0_fwd(const float* x, int B, int C, const float* W, int KK, const float* bias, float* y, void* stream);
 int cdm_up0_wgrad(const float* x, int B, int C, const float* dy, int KK, float* dW, void* stream);
+/* input gradient dx[n][ci] = sum_k dyT[n][k] W[ci][k] over k = (co, ij), dyT = dy transposed per sample to [B][C][KK]
+ * (B <= 16, C % 64 == 0): per-K-range partials slab [cdm_up0_dgrad_splits(C, KK)][B][C], folded by cdm_slab_reduce */
+int cdm_up0_dgrad(const float* dyT, int B, int C, const float* W, int KK, float* slab, void* stream);
+int cdm_up0_dgrad_splits(int C, int KK);
 
 #ifdef __cplusplus
 }

@@ -572,3 +572,24 @@ def test_cin1_wgrad_bn_backward_fused_bit_exact(L):
                                    H, C, 128, got.data_ptr(), _s())
     torch.cuda.synchronize()
     assert torch.isfinite(ref).all() and torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("B,C,k", [(1, 64, 16), (5, 128, 32), (16, 64, 64)])
+def test_up0_large_map_input_gradient(L, B, C, k):
+    """cdm_up0_dgrad (config-5 up0 input gradient over W in place, dy transposed per sample to [B][C][KK]) + the slab
+    fold vs torch CPU conv_transpose2d's input gradient in fp64, at the fp32 bar of this file."""
+    torch.manual_seed(12)
+    KK = k * k
+    x = torch.randn(B, C, 1, 1, dtype=torch.float64, requires_grad=True)
+    W = torch.randn(C, C, k, k, dtype=torch.float64) * 0.1
+    gy = torch.randn(B, C, k, k, dtype=torch.float64)
+    F.conv_transpose2d(x, W, None, stride=k).backward(gy)
+    dyT = gy.reshape(B, C, KK).float().contiguous().cuda()            # [B][co][ij]
+    Wc = W.float().cuda()
+    sp = L.raw("cdm_up0_dgrad_splits")(C, KK)
+    slab = torch.full((sp * B * C,), float("nan"), device="cuda")
+    L.cdm_up0_dgrad(dyT.data_ptr(), B, C, Wc.data_ptr(), KK, slab.data_ptr(), _s())
+    dx = torch.full((B, C), float("nan"), device="cuda")
+    L.cdm_slab_reduce(slab.data_ptr(), sp, B, C, dx.data_ptr(), C, 0, 1, C, 0, 1.0, _s())
+    torch.cuda.synchronize()
+    _close(dx, x.grad.reshape(B, C))
