@@ -524,55 +524,65 @@ CDM_API int cdm_reduce_stats(const float* y, int ldy, int N, int HW, int C, int 
 
 // cdm_reduce_stats (the same per-lane sums and fold order) + optional per-channel max / min of y as ordered-int keys
 // (atomic max into ymm[c], min into ymm[ymm_ld + c]): the BN statistics of the C_in = 1 init conv, whose train-mode
-// BN-ReLU apply then runs in the next conv's staging (bn_fwd_finalize turns the keys into the exact max|z|)
+// BN-ReLU apply then runs in the next conv's staging (bn_fwd_finalize turns the keys into the exact max|z|).
+// A block covers U0S_CG consecutive chunks of one image (one slab partial per chunk) and issues its max / min atomics
+// once: one block per chunk put 2 M atomics on the 2C key addresses at bs = 256 (~120 us of contention).
+constexpr int U0S_CG = 8;
 __global__ __launch_bounds__(256) void stats_mm_kernel(const float* __restrict__ y, int ldy, int HW, int C, int csize,
-                                                       float* __restrict__ slab, int* ymm, int ymm_ld) {
+                                                       int nchunks, float* __restrict__ slab, int* ymm, int ymm_ld) {
     __shared__ float red[256 * 4 * 2];
     __shared__ float rmx[256 * 4], rmn[256 * 4];
     const int C4 = C >> 2;
     const int P = 256 / C4;
     const int tid = threadIdx.x, c4 = tid % C4, pl = tid / C4;
-    const int n = blockIdx.y, chunk = blockIdx.x;
-    const int p0 = chunk * csize, p1 = min(HW, p0 + csize);
-    Acc4<2> a;
-    a.v[0] = f4zero(); a.v[1] = f4zero();
+    const int n = blockIdx.y;
     float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY), lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY);
-    const StatsF f{y, ldy, HW};
-    if (pl < P)
-        for (int p = p0 + pl; p < p1; p += P) {
-            f(n, p, c4 * 4, a);
-            const float4 v = ld4(y + ((long long)n * HW + p) * ldy + c4 * 4);
-            hi = make_float4(fmaxf(hi.x, v.x), fmaxf(hi.y, v.y), fmaxf(hi.z, v.z), fmaxf(hi.w, v.w));
-            lo = make_float4(fminf(lo.x, v.x), fminf(lo.y, v.y), fminf(lo.z, v.z), fminf(lo.w, v.w));
-        }
-    if (pl < P) {
+    const int cend = min(nchunks, (int)(blockIdx.x + 1) * U0S_CG);
+    for (int chunk = blockIdx.x * U0S_CG; chunk < cend; ++chunk) {
+        const int p0 = chunk * csize, p1 = min(HW, p0 + csize);
+        Acc4<2> a;
+        a.v[0] = f4zero(); a.v[1] = f4zero();
+        if (pl < P)
+            for (int p = p0 + pl; p < p1; p += P) {   // one read of y per element: StatsF's sums + max / min
+                const float4 v = ld4(y + ((long long)n * HW + p) * ldy + c4 * 4);
+                a.v[0].x += v.x; a.v[0].y += v.y; a.v[0].z += v.z; a.v[0].w += v.w;
+                a.v[1].x += v.x * v.x; a.v[1].y += v.y * v.y; a.v[1].z += v.z * v.z; a.v[1].w += v.w * v.w;
+                hi = make_float4(fmaxf(hi.x, v.x), fmaxf(hi.y, v.y), fmaxf(hi.z, v.z), fmaxf(hi.w, v.w));
+                lo = make_float4(fminf(lo.x, v.x), fminf(lo.y, v.y), fminf(lo.z, v.z), fminf(lo.w, v.w));
+            }
+        __syncthreads();   // red is reused per chunk
+        if (pl < P) {
 #pragma unroll
-        for (int r = 0; r < 2; ++r) st4(&red[(pl * 2 + r) * C + c4 * 4], a.v[r]);
+            for (int r = 0; r < 2; ++r) st4(&red[(pl * 2 + r) * C + c4 * 4], a.v[r]);
+        }
+        __syncthreads();
+        float* out = slab + ((long long)n * nchunks + chunk) * 2 * C;
+        for (int idx = tid; idx < 2 * C; idx += 256) {
+            float sacc = 0.f;
+            for (int q = 0; q < P; ++q) sacc += red[q * 2 * C + idx];
+            out[idx] = sacc;
+        }
+    }
+    if (!ymm) return;
+    if (pl < P) {
         st4(&rmx[pl * C + c4 * 4], hi);
         st4(&rmn[pl * C + c4 * 4], lo);
     }
     __syncthreads();
-    float* out = slab + ((long long)n * gridDim.x + chunk) * 2 * C;
-    for (int idx = tid; idx < 2 * C; idx += 256) {
-        float sacc = 0.f;
-        for (int q = 0; q < P; ++q) sacc += red[q * 2 * C + idx];
-        out[idx] = sacc;
+    for (int c = tid; c < C; c += 256) {
+        float mx = -INFINITY, mn = INFINITY;
+        for (int q = 0; q < P; ++q) { mx = fmaxf(mx, rmx[q * C + c]); mn = fminf(mn, rmn[q * C + c]); }
+        atomicMax(ymm + c, fkey(mx));
+        atomicMin(ymm + ymm_ld + c, fkey(mn));
     }
-    if (ymm)
-        for (int c = tid; c < C; c += 256) {
-            float mx = -INFINITY, mn = INFINITY;
-            for (int q = 0; q < P; ++q) { mx = fmaxf(mx, rmx[q * C + c]); mn = fminf(mn, rmn[q * C + c]); }
-            atomicMax(ymm + c, fkey(mx));
-            atomicMin(ymm + ymm_ld + c, fkey(mn));
-        }
 }
 
 CDM_API int cdm_reduce_stats_mm(const float* y, int ldy, int N, int HW, int C, int csize, float* slab, int* ymm,
                                 int ymm_ld, void* stream) {
     if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
     const int nchunks = (HW + csize - 1) / csize;
-    hipLaunchKernelGGL(stats_mm_kernel, dim3(nchunks, N), dim3(256), 0, S(stream), y, ldy, HW, C, csize, slab, ymm,
-                       ymm_ld);
+    hipLaunchKernelGGL(stats_mm_kernel, dim3((nchunks + U0S_CG - 1) / U0S_CG, N), dim3(256), 0, S(stream), y, ldy, HW,
+                       C, csize, nchunks, slab, ymm, ymm_ld);
     return cdm_status();
 }
 
