@@ -3,8 +3,9 @@
 Parameter tree, names, shapes, default initialisation order and therefore the seeded weights are
 identical to the reference, so ``state_dict()`` / ``load_state_dict()`` are interchangeable with
 checkpoints of the reference (156 entries incl. BatchNorm buffers).  The building blocks keep the
-reference constructor signatures (diffusion_utilities.py:13-145) and act as parameter holders:
-the network is executed as a whole by :class:`cdm_amd.engine.UNetEngine`.
+reference constructor signatures (diffusion_utilities.py:13-145); inside ContextUnet the network is executed as a
+whole by :class:`cdm_amd.engine.UNetEngine`, and a block called on its own runs a forward-only HIP path
+(:mod:`cdm_amd.blocks`).
 
 The reference draws a *fresh* random 1x1 shortcut convolution on every forward call
 (diffusion_utilities.py:54).  ``shortcut_source`` selects where that draw comes from:
@@ -32,9 +33,8 @@ def _conv_bn_relu(cin: int, cout: int) -> nn.Sequential:
 
 
 class _Holder(nn.Module):
-    def forward(self, *a, **k):  # pragma: no cover - explicit by design
-        raise RuntimeError(f"{type(self).__name__} is executed as part of ContextUnet on the HIP engine; "
-                           "call ContextUnet.forward")
+    """Inside ContextUnet the engine runs the network as a whole; a block called on its own runs its forward on the
+    HIP kernels (cdm_amd.blocks: forward only, fp32 convs, train / eval BatchNorm semantics)."""
 
 
 class ResidualConvBlock(_Holder):
@@ -47,8 +47,18 @@ class ResidualConvBlock(_Holder):
         self.conv1 = _conv_bn_relu(in_channels, out_channels)
         self.conv2 = _conv_bn_relu(out_channels, out_channels)
 
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from .blocks import residual_block_forward
+        return residual_block_forward(self, x)
+
     def get_out_channels(self):
         return self.conv2[0].out_channels
+
+    def set_out_channels(self, out_channels):
+        """diffusion_utilities.py:72-75: rewrites the conv attributes only (as the reference; weights keep their shape)."""
+        self.conv1[0].out_channels = out_channels
+        self.conv2[0].in_channels = out_channels
+        self.conv2[0].out_channels = out_channels
 
 
 class UnetUp(_Holder):
@@ -60,6 +70,10 @@ class UnetUp(_Holder):
                                    ResidualConvBlock(out_channels, out_channels),
                                    ResidualConvBlock(out_channels, out_channels))
 
+    def forward(self, x, skip):
+        from .blocks import unet_up_forward
+        return unet_up_forward(self, x, skip)
+
 
 class UnetDown(_Holder):
     """diffusion_utilities.py:103-116 — 2 conv blocks + MaxPool2d(2)."""
@@ -69,6 +83,10 @@ class UnetDown(_Holder):
         self.model = nn.Sequential(ResidualConvBlock(in_channels, out_channels),
                                    ResidualConvBlock(out_channels, out_channels), nn.MaxPool2d(2))
 
+    def forward(self, x):
+        from .blocks import unet_down_forward
+        return unet_down_forward(self, x)
+
 
 class EmbedFC(_Holder):
     """diffusion_utilities.py:118-145 — Linear(in,e) -> GELU -> Linear(e,e)."""
@@ -77,6 +95,10 @@ class EmbedFC(_Holder):
         super().__init__()
         self.input_dim = input_dim
         self.model = nn.Sequential(nn.Linear(input_dim, emb_dim), nn.GELU(), nn.Linear(emb_dim, emb_dim))
+
+    def forward(self, x):
+        from .blocks import embed_fc_forward
+        return embed_fc_forward(self, x)
 
 
 # ------------------------------------------------------------------------------------------------

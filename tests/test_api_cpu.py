@@ -90,3 +90,15 @@ def test_checkpoint_pth_round_trip(tmp_path, golden_dir):
     m2.load_state_dict(ref)
     for k, v in m2.state_dict().items():
         assert torch.equal(v, ref[k]), k
+
+
+def test_cpu_blocks_fail_loudly():
+    """The standalone block forwards run on the HIP kernels only (no CPU fallback)."""
+    from cdm_amd import EmbedFC, ResidualConvBlock, UnetDown
+    for mod, args in ((ResidualConvBlock(4, 8), (torch.zeros(1, 4, 8, 8),)), (UnetDown(4, 8), (torch.zeros(1, 4, 8, 8),)),
+                      (EmbedFC(6, 8), (torch.zeros(2, 6),))):
+        with pytest.raises(RuntimeError):
+            mod(*args)
+    blk = ResidualConvBlock(4, 8)
+    blk.set_out_channels(16)                      # diffusion_utilities.py:72-75: attributes only
+    assert blk.conv1[0].out_channels == blk.conv2[0].in_channels == blk.conv2[0].out_channels == 16
