@@ -159,8 +159,19 @@ def test_c4_bf16_cfg_sampler_vs_reference_golden(w):
     d = cdm_amd.DDPM(m, int(sfx["T"]), "cuda", z_source="host")
     torch.manual_seed(500)                       # the reference's RNG state for this trajectory
     x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(sfx["params"]), w)
-    assert _rel(x, torch.from_numpy(sfx[f"sample_w{w:g}"])) < 5e-2
-    assert _rel(torch.from_numpy(inter), torch.from_numpy(sfx[f"sample_w{w:g}_inter"])) < 5e-2
+    # bar: 1.5x the error of the reference's own sampler under the same bf16 operand rounding (the CPU oracle, which
+    # replays the reference's RNG order bit-exactly, with every 3x3 conv's operands rounded to bf16), at least 1e-3
+    T = int(sfx["T"])
+    with _bf16_operands():
+        torch.manual_seed(500)
+        xe, inte = R.sample_ddpm(R.make_model_fn(R.clone_sd(sd), n_feat=8, n_cfeat=6, height=64), 2, 64,
+                                 torch.from_numpy(sfx["params"]), w, T, R.make_schedule(T), 6)
+    gx, gi = torch.from_numpy(sfx[f"sample_w{w:g}"]), torch.from_numpy(sfx[f"sample_w{w:g}_inter"])
+    e_hip, e_emu = _rel(x, gx), _rel(xe, gx)
+    ei_hip, ei_emu = _rel(torch.from_numpy(inter), gi), _rel(inte, gi)
+    print(f"w={w:g}: final hip {e_hip:.2e} oracle-bf16 {e_emu:.2e}; snapshots hip {ei_hip:.2e} oracle-bf16 {ei_emu:.2e}")
+    assert e_hip <= max(1.5 * e_emu, 1e-3), (e_hip, e_emu)
+    assert ei_hip <= max(1.5 * ei_emu, 1e-3), (ei_hip, ei_emu)
 
 
 # ------------------------------------------------------------------------------------------ C5 (256x256)
