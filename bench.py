@@ -494,7 +494,7 @@ def main():
         }
         if extra:
             out["configs"] = extra
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:      # the CPU baseline is an N=1 leg (rank 0)
             out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
         print(json.dumps(out), flush=True)
     if dist is not None:
