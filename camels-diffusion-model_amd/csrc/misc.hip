@@ -249,10 +249,14 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_kernel(const float* z, int
 // reduces its halo pixels to the 9 per-tap partial sums s[tap][q] = sum_c z[q][c] w[c][tap] (the weights are
 // wave-uniform: scalar loads), and every output pixel then adds its 9 neighbours' partials.  z is read from
 // HBM once (+2/R halo rows) instead of 9 times through the caches.
+// gs / gt (optional, per (sample, channel) [N][C]): the input is relu(z gs + gt) of the pre-norm z (out.1's GroupNorm +
+// ReLU applied while staging, the fmaf of norm_apply_fwd: bit-identical to the applied tensor; padding stays zero)
 __global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* __restrict__ z, int ldz, int H, int W,
                                                                   int C, const float* __restrict__ w,
                                                                   const float* __restrict__ bias,
-                                                                  float* __restrict__ out) {
+                                                                  float* __restrict__ out,
+                                                                  const float* __restrict__ gs,
+                                                                  const float* __restrict__ gt) {
     constexpr int HPMAX = 512;                        // (R + 2) * W <= 256 + 2 * 128 for W <= 128; W = 256 -> 768
     __shared__ float zt[3 * 256 * 17];                // [halo px][16 ch + 1 pad]
     __shared__ float st[9 * 3 * 256];                 // [tap][halo px]
@@ -283,12 +287,23 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* _
     };
     gload(0);
     for (int c0 = 0; c0 < C; c0 += 16) {
+        float ks[4] = {1.f, 1.f, 1.f, 1.f}, kt[4] = {0.f, 0.f, 0.f, 0.f};
+        if (gs) {   // this thread's 4 channels (q4 & 3 == tid & 3 for every piece)
+            const int cb = n * C + c0 + (tid & 3) * 4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { ks[j] = gs[cb + j]; kt[j] = gt[cb + j]; }
+        }
 #pragma unroll
         for (int i = 0; i < PQ; ++i) {
             const int q4 = tid + i * 256;
             if ((q4 >> 2) < HP) {
+                float v[4] = {pre[i].x, pre[i].y, pre[i].z, pre[i].w};
+                if (gs && src[i]) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] = relu_f(fmaf(v[j], ks[j], kt[j]));
+                }
                 float* d = zt + (q4 >> 2) * 17 + (q4 & 3) * 4;
-                d[0] = pre[i].x; d[1] = pre[i].y; d[2] = pre[i].z; d[3] = pre[i].w;
+                d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
             }
         }
         __syncthreads();
@@ -835,11 +850,21 @@ CDM_API int cdm_conv3x3_cout1_fwd(const float* z, int ldz, int N, int H, int W, 
     const long long P = (long long)N * H * W;
     if (C % 16 == 0 && W <= 256 && 256 % W == 0 && H % (256 / W) == 0 && ldz % 4 == 0) {
         hipLaunchKernelGGL(conv_cout1_fwd_band_kernel, dim3(N * (H / (256 / W))), dim3(256), 0, S(stream), z, ldz, H, W,
-                           C, w, bias, out);
+                           C, w, bias, out, nullptr, nullptr);
         return cdm_status();
     }
     hipLaunchKernelGGL(conv_cout1_fwd_kernel, dim3(nblocks(P, 256 / (C / 4), 8192)), dim3(256), 0, S(stream), z, ldz, N, H,
                        W, C, w, bias, out);
+    return cdm_status();
+}
+// out.3 on out.1's pre-norm output y with its GroupNorm + ReLU (per (n, c) scale gs / shift gt, [N][C]) applied while
+// staging: the band form only (C % 16 == 0, W | 256, (256 / W) | H)
+CDM_API int cdm_conv3x3_cout1_fwd_gn(const float* y, int ldy, int N, int H, int W, int C, const float* gs,
+                                     const float* gt, const float* w, const float* bias, float* out, void* stream) {
+    if (C % 16 || C > 1024 || W > 256 || 256 % W || H % (256 / W) || ldy % 4 || !gs || !gt)
+        return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(conv_cout1_fwd_band_kernel, dim3(N * (H / (256 / W))), dim3(256), 0, S(stream), y, ldy, H, W, C, w,
+                       bias, out, gs, gt);
     return cdm_status();
 }
 CDM_API int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int C, const float* w, float* dz, int lddz,

@@ -445,6 +445,11 @@ class UNetEngine:
         self.conv3x3("out.0.wpk", ws.catO.p, B, H, 2 * nf, 2 * nf, _p(P["out.0.bias"]), _p(ws.yO), nf, nf, 0,
                      _p(ws.slab), nf, self.kc_out0, s, amax_x=self._slot(ws, "catO"))
         self._gn_fwd(ws, P, "out.1", Act(ws.yO, nf), B, H, nf, ws.gnO, stats_from_conv=True, stream=s)
+        if not train and nf % 16 == 0 and H <= 256 and 256 % H == 0:
+            # eval: out.1's GroupNorm + ReLU applied in out.3's staging (zO is only kept for the backward)
+            lb.cdm_conv3x3_cout1_fwd_gn(_p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]), _p(ws.gnO["shift"]),
+                                        _p(P["out.3.weight"]), _p(P["out.3.bias"]), _p(eps), s)
+            return eps
         lb.cdm_norm_apply_fwd(APPLY_RELU, _p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]), _p(ws.gnO["shift"]), nf,
                               None, 0, None, 0, None, None, None, 0, _p(ws.zO), nf, None, s)
         lb.cdm_conv3x3_cout1_fwd(_p(ws.zO), nf, B, H, H, nf, _p(P["out.3.weight"]), _p(P["out.3.bias"]), _p(eps), s)

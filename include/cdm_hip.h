@@ -235,6 +235,11 @@ int cdm_slab_sum_all(const double* part, int nparts, int R, int r0, int rn, int 
 /* out.3: Conv2d(nf, 1, 3, 1, 1) (ContextUnet.py:39) */
 int cdm_conv3x3_cout1_fwd(const float* z, int ldz, int N, int H, int W, int C, const float* w, const float* bias,
                           float* out, void* stream);
+/* out.3 on out.1's pre-norm output y with its GroupNorm + ReLU applied while staging (gs / gt per (sample, channel),
+ * [N][C]; bit-identical to cdm_norm_apply_fwd then cdm_conv3x3_cout1_fwd): eval forwards (ContextUnet.py:37-39).
+ * C % 16 == 0, W | 256, (256 / W) | H. */
+int cdm_conv3x3_cout1_fwd_gn(const float* y, int ldy, int N, int H, int W, int C, const float* gs, const float* gt,
+                             const float* w, const float* bias, float* out, void* stream);
 int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int C, const float* w, float* dz, int lddz,
                             void* stream);
 /* weight gradient partials: csize > 0: per (image, csize-pixel chunk) [N][chunks][9][C]; csize = -R (band form, H % R
