@@ -193,7 +193,7 @@ def _cpu_train_rate(R, nf: int, T: int, bs: int, steps: int, warmup: int):
     t0 = time.perf_counter()
     for _ in range(steps):
         one()
-    return (time.perf_counter() - t0) / steps, tr.sd
+    return (time.perf_counter() - t0) / max(steps, 1), tr.sd
 
 
 def _cpu_sample_rate(R, sd, nf: int, T: int, n: int, w: float, steps: int):
@@ -215,34 +215,62 @@ def _cpu_sample_rate(R, sd, nf: int, T: int, n: int, w: float, steps: int):
         else:
             eps = fn(x, t, params)
         x = R.denoise_add_noise(x, i, eps, z, b, a, ab)
-        if n > 8:
+        if n >= 32:
             _progress(f"cpu sample step n={n} w={w:g}")
     return (time.perf_counter() - t0) / steps
 
 
+def host_cpus():
+    """(os.cpu_count(), CPUs in this process's affinity mask, cgroup CPU quota or None)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return os.cpu_count(), aff, quota
+
+
+def usable_cpus() -> int:
+    """os.cpu_count(), capped by the affinity mask and the cgroup CPU quota: on the GPU box
+    os.cpu_count() reports the machine's 256 CPUs while the cgroup grants 16, and the oracle's train step runs 1.75x
+    slower on 32 threads than on 16 (profiles/r3_host_probe.txt), so more threads than the quota understate the host."""
+    cores, aff, quota = host_cpus()
+    n = min(cores, aff)
+    if quota:
+        n = min(n, max(1, int(quota)))
+    return n
+
+
 def cpu_baseline(threads: int):
     """The reference algorithm (CPU oracle = torch CPU fp32 restatement, pinned bit-exact to the reference's own
-    outputs) on the host cores, per BASELINE.md §3: C2 train step at bs=256 timed directly (1 warm-up + 2 steps),
-    3 sampling steps at n=256 for w=0 and w=1 extrapolated to T=1500, and config C1 (n_feat=64, bs=8, T=1000)."""
+    outputs) on the host cores, per BASELINE.md §3 (torch.set_num_threads(os.cpu_count()) unless --cpu-threads caps
+    it), a bounded sample of ~30 s of CPU work: the C2 train step at bs=256 timed directly (one step, after a bs=8
+    warm-up step), 2 sampling steps at n=32 for w=0 and w=1 extrapolated to T=1500 (per image), and config C1
+    (n_feat=64, bs=8, T=1000)."""
     from oracle import ref_cpu as R
+    cores, aff, quota = host_cpus()
     torch.set_num_threads(threads)
-    bs = 256
-    dt, sd = _cpu_train_rate(R, NF, T, bs, steps=2, warmup=1)
-    S = 3
-    s0 = _cpu_sample_rate(R, sd, NF, T, bs, 0.0, S)
-    s1 = _cpu_sample_rate(R, sd, NF, T, bs, 1.0, S)
+    bs, ns, S = 256, 32, 2
+    _cpu_train_rate(R, NF, T, 8, steps=0, warmup=1)                 # load the kernels / allocator at a small batch
+    dt, sd = _cpu_train_rate(R, NF, T, bs, steps=1, warmup=0)
+    s0 = _cpu_sample_rate(R, sd, NF, T, ns, 0.0, S)
+    s1 = _cpu_sample_rate(R, sd, NF, T, ns, 1.0, S)
     del sd
     # C1 (BASELINE.json configs[0]): n_feat=64, bs=8, T=1000
     T1 = 1000
     dt1, sd1 = _cpu_train_rate(R, 64, T1, 8, steps=5, warmup=1)
     s01 = _cpu_sample_rate(R, sd1, 64, T1, 8, 0.0, 10)
     return {
-        "value": bs / dt, "unit": "images/s", "cores": threads, "kind": "port",
-        "sample": f"C2 shape: 2 train steps (perturb + fwd + mse + bwd + Adam) at bs={bs}, n_feat=128, 64x64, timed "
-                  f"directly after 1 warm-up step; CPU oracle = torch CPU fp32 restatement of the reference path",
+        "value": bs / dt, "unit": "images/s", "cores": cores, "threads": threads, "affinity_cpus": aff,
+        "cgroup_cpu_quota": quota, "kind": "port",
+        "sample": f"C2 shape: 1 train step (perturb + fwd + mse + bwd + Adam) at bs={bs}, n_feat=128, 64x64, timed "
+                  f"directly after a bs=8 warm-up step; CPU oracle = torch CPU fp32 restatement of the reference path on "
+                  f"{threads} threads (os.cpu_count() = {cores}, affinity {aff}, cgroup quota {quota})",
         "ms_per_step": round(dt * 1e3, 1),
-        "sample_img_per_s_extrapolated": {"w=0": bs / (s0 * T), "w=1": bs / (s1 * T)},
-        "sample_note": f"{S} reverse-diffusion steps at n={bs} timed per guide weight ({s0 * 1e3:.0f} / "
+        "sample_img_per_s_extrapolated": {"w=0": ns / (s0 * T), "w=1": ns / (s1 * T)},
+        "sample_note": f"{S} reverse-diffusion steps at n={ns} timed per guide weight ({s0 * 1e3:.0f} / "
                        f"{s1 * 1e3:.0f} ms per step for w=0 / w=1) and extrapolated x{T} steps",
         "c1": {"workload": "C1: n_feat=64, 6 params, 64x64, T=1000, bs=8 (BASELINE configs[0], the reference's CPU "
                            "case)", "train_img_per_s": round(8 / dt1, 3), "train_ms_per_step": round(dt1 * 1e3, 1),
@@ -328,7 +356,7 @@ def extra_configs(args, barrier):
     torch.cuda.empty_cache()
     # C5: 256x256 maps, n_feat=256 (1.093 B params; up0 alone 1.07 B), T=2000, split-bf16 fp32-accurate convs
     B5, T5 = args.c5_batch, 2000
-    C5_TRAIN, C5_SAMPLE = 6, 60
+    C5_TRAIN, C5_SAMPLE = 6, 300
     model, ms, loss = train_rate(256, 256, T5, B5, args.conv_math, C5_TRAIN, 2, 0, barrier)
     _progress(f"C5 train {ms:.3f} ms/step")
     sms, S = sample_rate(model, T5, B5, 0.0, C5_SAMPLE, 0, barrier)
@@ -342,6 +370,46 @@ def extra_configs(args, barrier):
     del model
     torch.cuda.empty_cache()
     out["stats_pk_pdf"] = stats_rate(args.sample_batch)
+    return out
+
+
+def reference_logged_workloads(model, barrier):
+    """The reference's own logged GPU workloads on this path (…params_6/…/timing_and_performance.log):
+    NLL evaluation of 200 images x T=1500 no-grad forwards at bs=32 (calculate_likelihood, code/train_diffusion_elbo.py:
+    108-149; logged 364.16 s, :267) and T=1500 sampling of n=10 / n=25 images at w=0 (logged 19.38 s / 45.77 s,
+    :280-289) — full runs, nothing extrapolated; the C2 model (h3) on synthetic maps / parameters."""
+    from cdm_amd.likelihood import LikelihoodEvaluator
+    out = {}
+    g = torch.Generator().manual_seed(2024)
+    N, bs = 200, 32
+    x = torch.rand(N, 1, H, H, generator=g).cuda(); c = torch.rand(N, NCF, generator=g).cuda()
+    batches = [(x[i:i + bs], c[i:i + bs]) for i in range(0, N, bs)]
+    ev = LikelihoodEvaluator(model, T, "device")
+    ev._refresh()
+    for xb, cb in (batches[0], batches[-1]):          # capture the B=32 and the ragged B=8 graphs outside the timing
+        r = ev._run(xb.shape[0])
+        r.load(xb, cb)
+        r.capture(ev.K)
+    barrier()
+    t0 = time.perf_counter()
+    nll = ev.likelihood(batches)
+    barrier()
+    dt = time.perf_counter() - t0
+    _progress(f"NLL 200 x T=1500 {dt:.2f} s")
+    out["nll_200_T1500"] = {"workload": "calculate_likelihood of 200 maps (bs=32: 6 batches + 8), T=1500 eval forwards "
+                                        "each (code/train_diffusion_elbo.py:108-149)", "seconds": round(dt, 3),
+                            "img_fwd_per_s": round(N * T / dt, 1), "nll": nll, "reference_logged_s": 364.16,
+                            "reference_source": "graphs/conditional_lr_1e-05_epochs_100_timesteps_1500_params_6/"
+                                                "spectrum_lr_1e-05_epochs_100_timesteps_1500_params_6/"
+                                                "timing_and_performance.log:267 (one NVIDIA GPU, model unrecorded)"}
+    for n, logged, line in ((10, 19.38, 280), (25, 45.77, 289)):
+        ms, S = sample_rate(model, T, n, 0.0, T, 0, barrier)
+        _progress(f"sample n={n} T=1500 {ms:.3f} ms/step")
+        out[f"sample_n{n}_T1500"] = {"workload": f"sample_ddpm of {n} maps, T=1500, w=0 (full run)",
+                                     "seconds": round(ms * S * 1e-3, 3), "ms_per_denoise_step": round(ms, 3),
+                                     "img_per_s": round(n / (ms * S * 1e-3), 3), "steps_run": S,
+                                     "reference_logged_s": logged,
+                                     "reference_source": f"same log :{line}"}
     return out
 
 
@@ -387,14 +455,16 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--sample-steps", type=int, default=T, help="sampling steps actually run (T=1500 = full)")
     ap.add_argument("--sample-batch", type=int, default=256)
-    ap.add_argument("--cfg-sample-steps", type=int, default=300,
-                    help="steps run for the C2 CFG (w=1,3) sampling rates (extrapolated to T)")
-    ap.add_argument("--extra-sample-steps", type=int, default=300, help="sampling steps of the C4 legs")
+    ap.add_argument("--cfg-sample-steps", type=int, default=T,
+                    help="steps run for the C2 CFG (w=1,3) sampling rates (T = full runs)")
+    ap.add_argument("--extra-sample-steps", type=int, default=T, help="sampling steps of the C4 legs (T = full runs)")
     ap.add_argument("--c5-batch", type=int, default=16)
     ap.add_argument("--no-extra", action="store_true", help="skip the C4 / C5 legs")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0 = the CPUs this process may use: os.cpu_count() within the affinity "
+                         "mask and the cgroup CPU quota)")
     ap.add_argument("--conv-math", choices=sorted(CONV_MATH_INFO), default="h3",
                     help="3x3 conv arithmetic of the C2 / C5 legs (fp32-accurate; see DESIGN.md §3)")
     args = ap.parse_args()
@@ -438,6 +508,7 @@ def main():
         _progress(f"C2 sample w={w:g} {cms:.3f} ms/step")
         cfg[f"w={w:g}"] = {"ms_per_denoise_step": round(cms, 3), "steps_run": CS,
                            "img_per_s": round(world * n / (cms * 1e-3 * T), 4), "extrapolated_to_T": CS < T}
+    logged = reference_logged_workloads(model, barrier) if (world == 1 and not args.no_extra) else None
     del model
     torch.cuda.empty_cache()
 
@@ -494,8 +565,10 @@ def main():
         }
         if extra:
             out["configs"] = extra
+        if logged:
+            out["reference_logged_workloads"] = logged
         if not args.no_cpu and world == 1:      # the CPU baseline is an N=1 leg (rank 0)
-            out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_threads or usable_cpus())
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

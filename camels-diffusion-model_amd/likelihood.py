@@ -127,12 +127,14 @@ class LikelihoodEvaluator:
     """Holds the schedule tables, the per-batch-size runs and graphs of one model."""
 
     def __init__(self, model, timesteps: int, noise_source: str = "device", steps_per_graph: int = 10,
-                 seed: int = 4321, use_graph: bool = True):
+                 seed: int = 4321, use_graph: bool = True, sched_tensors=None):
+        """``sched_tensors=(b_t, a_t, ab_t)``: the caller's schedule (the reference functions take them as
+        arguments and use them as given); None builds the default schedule of the training scripts."""
         assert noise_source in ("device", "host")
         self.model, self.T = model, int(timesteps)
         self.eng, self.P = model._engine_and_params()
         self.dev = self.P["out.3.weight"].device
-        self.sched = Schedule(self.T, self.dev)
+        self.sched = Schedule(self.T, self.dev, tensors=sched_tensors)
         self.noise_source = noise_source
         self.seed = seed
         self.K = max(1, int(steps_per_graph))
@@ -240,19 +242,38 @@ class LikelihoodEvaluator:
         return avg, avg / (64 * 64 * math.log(2))
 
 
-def _evaluator(model, timesteps, noise_source="device") -> LikelihoodEvaluator:
+def _sched_tensors(timesteps, ab_t, b_t, a_t):
+    """The caller's schedule as (b_t, a_t, ab_t) fp32 host tensors, or None for the default one.  The reference
+    reads ab_t (and b_t) exactly as passed (code/train_diffusion_elbo.py:130,140; code/train_diffusion_paper.py:
+    111,122); a missing a_t (unused by both estimators) is derived as 1 - b_t."""
+    if ab_t is None and b_t is None and a_t is None:
+        return None
+    if ab_t is None or b_t is None:
+        raise ValueError("pass ab_t and b_t (the tensors the estimators read) or none of the schedule tensors")
+    b = torch.as_tensor(b_t).detach().to("cpu", torch.float32).reshape(-1)
+    a = (1 - b) if a_t is None else torch.as_tensor(a_t).detach().to("cpu", torch.float32).reshape(-1)
+    ab = torch.as_tensor(ab_t).detach().to("cpu", torch.float32).reshape(-1)
+    if not (b.numel() == a.numel() == ab.numel() == int(timesteps) + 1):
+        raise ValueError(f"schedule tensors must have timesteps + 1 = {int(timesteps) + 1} entries")
+    return b, a, ab
+
+
+def _evaluator(model, timesteps, noise_source="device", sched=None) -> LikelihoodEvaluator:
     cache = model.__dict__.setdefault("_cdm_lik_eval", {})
-    key = (int(timesteps), noise_source)
+    skey = None if sched is None else tuple(v.numpy().tobytes() for v in sched)
+    key = (int(timesteps), noise_source, skey)
     ev = cache.get(key)
     if ev is None:
-        ev = cache[key] = LikelihoodEvaluator(model, timesteps, noise_source)
+        ev = cache[key] = LikelihoodEvaluator(model, timesteps, noise_source, sched_tensors=sched)
     return ev
 
 
 def calculate_likelihood(model, dataloader, timesteps, device=None, ab_t=None, b_t=None, a_t=None,
                          noise_source: str = "device") -> float:
-    """code/train_diffusion_elbo.py:108-149 — mean negative log likelihood (the reference's approximation)."""
-    return _evaluator(model, timesteps, noise_source).likelihood(dataloader)
+    """code/train_diffusion_elbo.py:108-149 — mean negative log likelihood (the reference's approximation), under
+    the caller's schedule ab_t / b_t when given."""
+    sched = _sched_tensors(timesteps, ab_t, b_t, a_t)
+    return _evaluator(model, timesteps, noise_source, sched).likelihood(dataloader)
 
 
 def calculate_elbo_and_bpd_batch(x, pred_noise, noise, t, b_t, a_t, ab_t, dims):
@@ -274,8 +295,10 @@ def calculate_elbo_and_bpd_batch(x, pred_noise, noise, t, b_t, a_t, ab_t, dims):
 
 def calculate_elbo_and_bpd_dataset(model, dataloader, timesteps, device=None, ab_t=None, b_t=None, a_t=None,
                                    noise_source: str = "device"):
-    """code/train_diffusion_paper.py:77-139 — (avg_elbo, bpd) over a dataset."""
-    return _evaluator(model, timesteps, noise_source).elbo_and_bpd(dataloader)
+    """code/train_diffusion_paper.py:77-139 — (avg_elbo, bpd) over a dataset, under the caller's schedule when
+    given."""
+    sched = _sched_tensors(timesteps, ab_t, b_t, a_t)
+    return _evaluator(model, timesteps, noise_source, sched).elbo_and_bpd(dataloader)
 
 
 def calculate_elbo_and_bpd(*args, **kwargs):

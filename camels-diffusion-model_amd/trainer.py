@@ -80,7 +80,9 @@ class GradBucketer:
 
 class Trainer:
     def __init__(self, model, lrate: float, timesteps: int, batch_size: int, seed: int = 0,
-                 use_graph: bool = True, group=None, broadcast_buffers: bool = True):
+                 use_graph: bool = True, group=None, broadcast_buffers: bool = True, force_ddp: bool = False):
+        """``force_ddp``: take the data-parallel path (stage-bucketed async all-reduce, rank-0 broadcasts, eager
+        steps) even in a one-rank process group — RCCL readiness on a one-GPU box (tests/test_gpu_rccl.py)."""
         self.model = model
         eng, P = model._engine_and_params()
         self.eng = eng
@@ -90,7 +92,7 @@ class Trainer:
         self.H, self.nf, self.ncf = model.h, model.n_feat, model.n_cfeat
         self.group = group
         import torch.distributed as dist
-        self.ddp = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.ddp = dist.is_available() and dist.is_initialized() and (dist.get_world_size(group) > 1 or force_ddp)
         self.world = dist.get_world_size(group) if self.ddp else 1
         self.seed = int(seed)
         # ---- flat parameter / gradient / moment buffers in backward-completion order ----

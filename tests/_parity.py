@@ -1,0 +1,30 @@
+"""Measured parity errors of the GPU tests, recorded for the round's profiles/ (e.g. profiles/r3_parity.json).
+
+Tests call record(name, **values) with the errors they assert on and the bars they hold them to; when $CDM_PARITY_OUT
+names a file, each record is appended to it as one JSON line (the GPU run writes it under gpurun_out/, then it is
+copied into profiles/).  Without the variable nothing is written."""
+import json
+import os
+
+
+def _plain(v):
+    try:
+        import numpy as np
+        if isinstance(v, np.generic):
+            return v.item()
+    except ImportError:
+        pass
+    if isinstance(v, dict):
+        return {str(k): _plain(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [_plain(x) for x in v]
+    return v
+
+
+def record(name: str, **values):
+    path = os.environ.get("CDM_PARITY_OUT")
+    if not path:
+        return
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "a") as f:
+        f.write(json.dumps({"test": name, **_plain(values)}) + "\n")

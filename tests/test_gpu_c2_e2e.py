@@ -1,0 +1,242 @@
+"""End-to-end parity of the benchmarked C2 configuration: the Trainer step bench.py times, at its own shape.
+
+n_feat=128, 6 params, 64x64, **B=256**, T=1500, h3 arithmetic, hipGraph replay — the exact first two steps of
+bench.py's C2 leg (seeded init torch.manual_seed(0), x0 / c from the CUDA generator 1234, Trainer seed 0, lr 1e-5,
+Philox noise / t / 1x1 shortcut drawn on device).  The draws each step used are read back from the Trainer's device
+buffers and handed to the CPU oracle (code/train_diffusion_condition.py:216-229: perturb_input, ContextUnet in train
+mode, F.mse_loss, backward, Adam), so the whole bench-shape chain is pinned end to end: BatchNorm batch statistics over
+1,048,576 pixels per channel (bn_fwd_finalize), the 14 fused BN-backward layers at 4,096 tiles, the split-K slab folds,
+the fused Adam, the graph replay.
+
+Step 1 (the eager first step of the bench) against the oracle from the same seeded weights and draws:
+  vs fp32 (the reference's arithmetic; a full oracle train step is ~20 s on the box host):
+    eps (train-mode forward)    max|d| <= 2e-4 max|eps|   (the whole-model forward bar, test_gpu_model.py)
+    loss                        |d| <= 1e-5 |loss|
+    every parameter gradient    relative L2 <= 1e-2 per tensor, median over tensors <= 5e-3 (the bar of
+                                test_gpu_model.py:149-198; conv biases feeding a BatchNorm: |g| <= 1e-4 max|g|)
+    parameters after Adam       |dp| / lr: RMS and 99th percentile <= 0.1 (Adam's first step moves every parameter
+                                by ~lr sign(g): a deviation is a sign decision on a gradient below rounding);
+                                BN-fed conv biases <= 2 lr
+    fused Adam                  == the restatement of torch.optim.Adam (oracle.adam_step_restated) on >= 99.999 %,
+                                moments bit-identical
+  vs fp64, forward only (~35 s): eps, loss and BatchNorm running statistics within 3x the reference's own fp32
+    deviation (eps: at least 2e-5 max|eps|; loss: + 1e-6 |loss|; statistics: + 1e-5 max|stat| + 1e-7).
+Step 2 (hipGraph replay) against the fp32 oracle run from the HIP state after step 1 (same parameters, running
+statistics, draws): eps, loss and gradients at the bars above, Adam against the restatement.
+Every test stays well under two minutes (no silent stretch for the GPU harness).
+Measured values are written to $CDM_PARITY_OUT (profiles/r3_parity.json).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu as R
+import _parity
+
+pytestmark = pytest.mark.gpu
+NF, NCF, H, B, T, LR = 128, 6, 64, 256, 1500, 1e-5
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.set_num_threads(min(16, max(1, len(__import__("os").sched_getaffinity(0)))))
+
+
+def _bn_fed_bias(k):
+    return ".conv1.0.bias" in k or ".conv2.0.bias" in k
+
+
+_HIP = {}
+
+
+def _flat_views(tr, flat):
+    out = {}
+    for n, view in tr.views.items():
+        lo = (view.data_ptr() - tr.flat.data_ptr()) // 4
+        out[n] = flat[lo:lo + view.numel()].view_as(view)
+    return out
+
+
+def _hip_steps():
+    """Two bench-identical Trainer steps; per step: draws, eps, loss, gradients, parameters / moments before and after,
+    running statistics."""
+    if _HIP:
+        return _HIP
+    from cdm_amd import ContextUnet, Trainer
+    torch.manual_seed(0)
+    m = ContextUnet(1, NF, NCF, H, shortcut_source="device", conv_math="h3").cuda()
+    sd0 = R.clone_sd(m.state_dict())
+    tr = Trainer(m, LR, T, B, seed=0, use_graph=True)
+    g = torch.Generator(device="cuda").manual_seed(1234)
+    x0 = torch.rand(B, 1, H, H, device="cuda", generator=g)
+    c = torch.rand(B, NCF, device="cuda", generator=g)
+    steps = []
+    for k in range(2):
+        pre = (tr.flat.cpu(), tr.m.cpu(), tr.v.cpu())
+        loss = float(tr.step(x0, c).item())
+        torch.cuda.synchronize()
+        sb = tr.cur
+        steps.append(dict(
+            step=k + 1, replay=tr.graph is not None and k == 1, loss=loss,
+            noise=sb.noise.view(B, 1, H, H).cpu().clone(), t=sb.t_int.cpu().long().clone(), sc=tr.sc.cpu().clone(),
+            eps=sb.ws.eps.view(B, 1, H, H).cpu().clone(), gflat=tr.gflat.cpu().clone(),
+            pre=pre, post=(tr.flat.cpu(), tr.m.cpu(), tr.v.cpu()),
+            sd={kk: v.detach().cpu().clone() for kk, v in m.state_dict().items()}))
+    assert steps[1]["replay"], "step 2 must be the captured graph's replay"
+    _HIP.update(sd0=sd0, x=x0.cpu(), c=c.cpu(), steps=steps, tr=tr)
+    return _HIP
+
+
+def _grads(tr, gflat):
+    return {n: v.clone() for n, v in _flat_views(tr, gflat).items()}
+
+
+def _oracle_step(sd, x, c, st, dtype):
+    s = {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+    otr = R.OracleTrainer(s, n_feat=NF, n_cfeat=NCF, height=H, lr=LR)
+    _, _, ab = R.make_schedule(T)
+    w = st["sc"][:NF].reshape(NF, 1, 1, 1).to(dtype); b = st["sc"][NF:].to(dtype)
+    loss, pred, grads = otr.step(x.to(dtype), c.to(dtype), st["noise"].to(dtype), st["t"], T, ab.to(dtype), (w, b))
+    post = {k: v.detach().clone() for k, v in otr.sd.items()}
+    return float(loss), pred, grads, post
+
+
+def _grad_errs(got, ref, ref32=None):
+    gmax = max(v.abs().max().item() for v in ref.values())
+    errs, errs32, zero = {}, {}, {}
+    for n, r in ref.items():
+        v = got[n].double()
+        if _bn_fed_bias(n):
+            zero[n] = v.abs().max().item() / gmax
+            continue
+        errs[n] = ((v - r.double()).norm() / r.double().norm()).item()
+        if ref32 is not None:
+            errs32[n] = ((ref32[n].double() - r.double()).norm() / r.double().norm()).item()
+    return errs, errs32, zero
+
+
+def _adam_exact(tr, st):
+    p0, m0, v0 = (a.numpy() for a in st["pre"])
+    p1, m1, v1 = (a.numpy() for a in st["post"])
+    rp, rm, rv = R.adam_step_restated(p0, st["gflat"].numpy(), m0, v0, LR, st["step"])
+    return float((p1 == rp).mean()), bool(np.array_equal(m1, rm) and np.array_equal(v1, rv))
+
+
+_ORACLE1 = {}
+
+
+def _oracle_step1(dtype):
+    """The oracle's step 1 from the seeded weights with HIP's step-1 draws (cached: fp32 ~20 s, fp64 ~100 s on the
+    box host)."""
+    if dtype not in _ORACLE1:
+        hip = _hip_steps()
+        _ORACLE1[dtype] = _oracle_step(hip["sd0"], hip["x"], hip["c"], hip["steps"][0], dtype)
+    return _ORACLE1[dtype]
+
+
+def _oracle_forward64(sd, x, c, st):
+    """The train-mode forward alone in fp64 (eps, loss, BatchNorm running statistics): one third of a step's cost, so
+    the test stays well inside a minute on the box host."""
+    s = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+    _, _, ab = R.make_schedule(T)
+    w = st["sc"][:NF].reshape(NF, 1, 1, 1).double(); b = st["sc"][NF:].double()
+    with torch.no_grad():
+        xp = R.perturb_input(x.double(), st["t"], st["noise"].double(), ab.double())
+        pred = R.unet_forward(s, xp, st["t"] / T, c.double(), n_feat=NF, n_cfeat=NCF, height=H, train=True,
+                              shortcut=(w, b))
+        loss = torch.nn.functional.mse_loss(pred, st["noise"].double())
+    return float(loss), pred, s
+
+
+def test_c2_step1_vs_fp32_oracle():
+    """Step 1 at the bench shape vs the fp32 oracle (the reference's arithmetic): eps, loss, every gradient, the
+    parameters after Adam, the fused Adam itself."""
+    hip = _hip_steps()
+    st = hip["steps"][0]
+    tr = hip["tr"]
+    l32, p32, g32, sd32 = _oracle_step1(torch.float32)
+    mx = p32.abs().max().item()
+    e_eps = (st["eps"] - p32).abs().max().item() / mx
+    e_loss = abs(st["loss"] - l32)
+    errs, _, zero = _grad_errs(_grads(tr, st["gflat"]), g32)
+    worst = max(errs, key=errs.get)
+    # parameters after Adam in units of lr (step one of Adam moves every parameter by ~lr sign(g): a deviation is a
+    # sign decision on a gradient below the two paths' rounding difference)
+    keep = [n for n in tr.views if not _bn_fed_bias(n)]
+    post = _flat_views(tr, st["post"][0])
+    d = np.concatenate([((post[n].double() - sd32[n].double()) / LR).abs().numpy().ravel() for n in keep])
+    d_rms, d_p99, d_frac = float(np.sqrt((d ** 2).mean())), float(np.percentile(d, 99)), float((d > 0.5).mean())
+    bias_dev = max((post[n] - sd32[n]).abs().max().item() for n in tr.views if _bn_fed_bias(n))
+    adam_frac, moments_exact = _adam_exact(tr, st)
+    med = float(np.median(list(errs.values())))
+    _parity.record("c2_e2e_step1_vs_fp32", B=B, n_feat=NF, conv_math="h3", loss=st["loss"], loss_oracle=l32,
+                   eps_err=e_eps, loss_err=e_loss, grad_rel_l2_max=errs[worst], grad_rel_l2_max_tensor=worst,
+                   grad_rel_l2_median=med, bn_fed_bias_max_rel=max(zero.values()), param_dev_lr_rms=d_rms,
+                   param_dev_lr_p99=d_p99, param_frac_dev_over_half_lr=d_frac, bn_fed_bias_dev_lr=bias_dev / LR,
+                   adam_exact_frac=adam_frac, adam_moments_exact=moments_exact)
+    print(f"C2 step 1 vs fp32: eps {e_eps:.2e}; loss {st['loss']:.7f} vs {l32:.7f}; grads max {errs[worst]:.2e} "
+          f"({worst}) median {med:.2e}; |dp|/lr rms {d_rms:.2e} p99 {d_p99:.2e} (> lr/2: {d_frac:.2e}); "
+          f"Adam exact {adam_frac:.6f}")
+    assert e_eps <= 2e-4
+    assert e_loss <= 1e-5 * abs(l32)
+    assert errs[worst] <= 1e-2 and med <= 5e-3, worst
+    assert max(zero.values()) <= 1e-4
+    assert d_rms <= 0.1 and d_p99 <= 0.1
+    assert bias_dev <= 2 * LR + 1e-9
+    assert adam_frac >= 0.99999 and moments_exact
+
+
+def test_c2_step1_forward_vs_fp64_oracle():
+    """Step 1's train-mode forward at the bench shape vs the oracle in fp64, next to the reference's own fp32
+    deviation: eps, loss, BatchNorm running statistics over 1,048,576 pixels per channel."""
+    hip = _hip_steps()
+    st = hip["steps"][0]
+    l64, p64, sd64 = _oracle_forward64(hip["sd0"], hip["x"], hip["c"], st)
+    l32, p32, _, sd32 = _oracle_step1(torch.float32)
+    mx = p64.abs().max().item()
+    e_eps, e_eps32 = (st["eps"].double() - p64).abs().max().item() / mx, (p32.double() - p64).abs().max().item() / mx
+    e_loss, e_loss32 = abs(st["loss"] - l64), abs(l32 - l64)
+    e_bn, e_bn32, bn_ok = 0.0, 0.0, True
+    for k, v in st["sd"].items():
+        if "running" in k:
+            eh = (v.double() - sd64[k]).abs().max().item(); er = (sd32[k].double() - sd64[k]).abs().max().item()
+            bn_ok &= eh <= 3 * er + 1e-5 * sd64[k].abs().max().item() + 1e-7
+            e_bn, e_bn32 = max(e_bn, eh), max(e_bn32, er)
+        elif k.endswith("num_batches_tracked"):
+            assert int(v) == 1, k
+    _parity.record("c2_e2e_step1_forward_vs_fp64", B=B, n_feat=NF, conv_math="h3", eps_err=e_eps,
+                   eps_err_ref32=e_eps32, loss_err=e_loss, loss_err_ref32=e_loss32, bn_running_err=e_bn,
+                   bn_running_err_ref32=e_bn32)
+    print(f"C2 step 1 forward vs fp64: eps {e_eps:.2e} (reference fp32 {e_eps32:.2e}); loss err {e_loss:.2e} "
+          f"(reference fp32 {e_loss32:.2e}); BN running {e_bn:.2e} (reference fp32 {e_bn32:.2e})")
+    assert e_eps <= max(3 * e_eps32, 2e-5)
+    assert e_loss <= 3 * e_loss32 + 1e-6 * abs(l64)
+    assert bn_ok
+
+
+def test_c2_step2_graph_replay_vs_oracle():
+    """Step 2 (the captured graph's replay, the steady state bench.py times) vs the fp32 oracle from the same state."""
+    hip = _hip_steps()
+    st1, st2 = hip["steps"]
+    tr = hip["tr"]
+    sd = {k: v.clone() for k, v in st1["sd"].items()}          # HIP parameters + running stats after step 1
+    l32, p32, g32, _ = _oracle_step(sd, hip["x"], hip["c"], st2, torch.float32)
+    mx = p32.abs().max().item()
+    e_eps = (st2["eps"] - p32).abs().max().item() / mx
+    e_loss = abs(st2["loss"] - l32)
+    errs, _, zero = _grad_errs(_grads(tr, st2["gflat"]), g32)
+    worst = max(errs, key=errs.get)
+    adam_frac, moments_exact = _adam_exact(tr, st2)
+    _parity.record("c2_e2e_step2_replay_vs_fp32", B=B, n_feat=NF, conv_math="h3", loss=st2["loss"], loss32=l32,
+                   eps_err=e_eps, loss_err=e_loss, grad_rel_l2_max=errs[worst], grad_rel_l2_max_tensor=worst,
+                   grad_rel_l2_median=float(np.median(list(errs.values()))), bn_fed_bias_max_rel=max(zero.values()),
+                   adam_exact_frac=adam_frac, adam_moments_exact=moments_exact)
+    print(f"C2 step 2 (replay): eps {e_eps:.2e}; loss {st2['loss']:.7f} vs {l32:.7f}; grads max {errs[worst]:.2e} "
+          f"({worst}) median {np.median(list(errs.values())):.2e}; Adam exact {adam_frac:.6f}")
+    assert e_eps <= 2e-4
+    assert e_loss <= 1e-5 * abs(l32)
+    assert errs[worst] <= 1e-2 and float(np.median(list(errs.values()))) <= 5e-3, worst
+    assert max(zero.values()) <= 1e-4
+    assert adam_frac >= 0.99999 and moments_exact

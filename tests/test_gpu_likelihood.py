@@ -104,3 +104,38 @@ def test_likelihood_graph_equals_eager_device_rng():
         assert ev.rng_ctr.item() == 25
     assert torch.isfinite(out[0]).all() and (out[0] > 0).all()
     assert torch.equal(out[0], out[1])
+
+
+def test_caller_schedule_is_used():
+    """calculate_likelihood / calculate_elbo_and_bpd(model, loader, T, device, ab_t, b_t, a_t) read the caller's
+    schedule tensors as the reference does (code/train_diffusion_elbo.py:130,140; code/train_diffusion_paper.py:
+    111,122): a non-default schedule (beta 2e-4 .. 0.03, cumprod instead of exp-cumsum-log) against the oracle under
+    the same tensors (host RNG, 1e-4 rel), and a different result from the default schedule."""
+    import cdm_amd
+    torch.manual_seed(4)
+    m = cdm_amd.ContextUnet(1, 16, 6, 64).cuda().eval()
+    sd = R.clone_sd(m.state_dict())
+    g = torch.Generator().manual_seed(6)
+    batches = [(torch.rand(3, 1, 64, 64, generator=g), torch.rand(3, 6, generator=g))]
+    T = 12
+    b = (0.03 - 2e-4) * torch.linspace(0, 1, T + 1) + 2e-4
+    a = 1 - b
+    ab = torch.cumprod(a, 0)
+    ab[0] = 1
+    fn = R.make_model_fn(sd, n_feat=16, n_cfeat=6, height=64)
+    torch.manual_seed(78)
+    got = cdm_amd.calculate_likelihood(m, batches, T, "cuda", ab.cuda(), b.cuda(), a.cuda(), noise_source="host")
+    torch.manual_seed(78)
+    ref = R.calculate_likelihood(fn, batches, T, (b, a, ab))
+    _close(got, ref, 1e-4)
+    torch.manual_seed(78)
+    default = cdm_amd.calculate_likelihood(m, batches, T, "cuda", noise_source="host")
+    assert abs(default - got) > 1e-2 * abs(ref), (default, got)
+    torch.manual_seed(79)
+    e, bp = cdm_amd.calculate_elbo_and_bpd(m, batches, T, "cuda", ab, b, a, noise_source="host")
+    torch.manual_seed(79)
+    e_ref, bp_ref = R.calculate_elbo_and_bpd_dataset(fn, batches, T, (b, a, ab))
+    _close(e, e_ref, 1e-4)
+    _close(bp, bp_ref, 1e-4)
+    with pytest.raises(ValueError):
+        cdm_amd.calculate_likelihood(m, batches, T, "cuda", ab[:-1], b[:-1], a[:-1])

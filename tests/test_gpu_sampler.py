@@ -12,6 +12,7 @@ import pytest
 import torch
 
 from oracle import ref_cpu as R
+import _parity
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -114,9 +115,13 @@ def test_sample_T1500_matches_reference(w, math):
     """sample_ddpm at T=1500 (code/train_diffusion_condition.py:281-335), CPU-RNG replay (z_source="host").
 
     Tolerance relative to max|x| (errors scale with |x|, which reaches ~1e4 with these untrained
-    weights): the reference's own fp32 run deviates from the same trajectory in fp64 by 3.5e-6 (w=0) / 3.9e-6
-    (w=3) of max|x|; the HIP run must stay within 1e-4 of max|x| of the fp64 trajectory (~30x that), for the
-    final x and every stored snapshot."""
+    weights), anchored on the reference's own fp32 deviation from the same trajectory run in fp64 (3.5e-6 (w=0) /
+    3.9e-6 (w=3) of max|x| at the end): for the final x and every stored snapshot, the HIP deviation from fp64 must
+    stay within 3x the reference's fp32 deviation at that snapshot plus a floor of 2e-6 max|x| (the reference's
+    deviation after ~1/3 of the trajectory; snapshots near x_T have deviations of 1e-7, where a fixed multiple of
+    the reference's error would be a bar below one fp32 rounding of the 1e4-sized values).  Measured (GPU box,
+    profiles/r3_parity.json): HIP 1.06e-5 / 9.8e-6 of max|x| at the end, 2.5-3.0x the reference's (identical under
+    h3 and the fp32 MFMA: the residual is not the 3x3-conv arithmetic)."""
     import cdm_amd
     sfx = np.load(os.path.join(GOLD, "sampler_T1500_nf8.npz"))
     T = int(sfx["T"])
@@ -136,11 +141,18 @@ def test_sample_T1500_matches_reference(w, math):
     e_hip, e_ref = np.abs(x - ref64).max() / mx, np.abs(ref32 - ref64).max() / mx
     print(f"T=1500 w={w:g} [{math}]: max|x| {mx:.3g}; vs fp64: HIP {e_hip:.2e}, reference fp32 {e_ref:.2e}; "
           f"HIP vs reference fp32 {np.abs(x - ref32).max() / mx:.2e}")
-    assert e_hip <= 1e-4
     keep = sfx["snap_keep"]
+    snaps = []
     for j, s in enumerate(keep):
         r = sfx[f"w{w:g}_inter_fp64"][j]
-        assert np.abs(inter[s] - r).max() <= 1e-4 * np.abs(r).max(), f"snapshot {s}"
+        rm = np.abs(r).max()
+        snaps.append((int(s), float(np.abs(inter[s] - r).max() / rm), float(np.abs(sfx[f"w{w:g}_inter"][j] - r).max() / rm)))
+    _parity.record("sample_T1500", w=w, conv_math=math, max_abs_x=float(mx), final_err=float(e_hip),
+                   final_err_ref32=float(e_ref), snapshots=[{"slot": a, "err": b, "err_ref32": c} for a, b, c in snaps])
+    floor = 2e-6
+    assert e_hip <= 3 * e_ref + floor, (e_hip, e_ref)
+    for s, e, er in snaps:
+        assert e <= 3 * er + floor, f"snapshot {s}: {e:.3e} vs reference {er:.3e}"
 
 
 def test_device_z_fresh_per_call_and_seedable():
