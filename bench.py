@@ -339,12 +339,19 @@ def extra_configs(args, barrier):
     single GPU, shortened runs (step counts stated in the output)."""
     out = {}
     # C4: bf16 MFMA operands, fp32 accumulate / master weights / activations; CFG w in {0,1,3}
-    model, ms, loss = train_rate(NF, H, T, args.batch, "bf16", 10, 3, 0, barrier)
+    model, ms, loss, (cms4, cn4) = train_rate(NF, H, T, args.batch, "bf16", 10, 3, 0, barrier, conv_probe=True)
     _progress(f"C4 train {ms:.3f} ms/step")
+    c4_tf = CONV_GFLOP_PER_IMG * args.batch / (cms4 * 1e-3) / 1e3
     c4 = {"workload": "C4: ContextUnet n_feat=128 64x64, bf16 mixed-precision convs (bf16 operands, fp32 "
                       "accumulate, fp32 master weights / activations / norms), T=1500",
           "batch": args.batch, "train_img_per_s": round(args.batch / (ms * 1e-3), 2), "train_ms_per_step": round(ms, 3),
-          "train_steps": 10, "final_loss": loss, "sample": {}}
+          "train_steps": 10, "final_loss": loss,
+          "roofline": {"bound": "mfma", "kernel": "conv3x3 128->128 @64x64 fwd (conv3x3_halo_x3_kernel<1,64>, bf16)",
+                       "achieved": round(c4_tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                       "frac": round(c4_tf / PEAK_BF16_TFLOPS, 4), "launch_ms": round(cms4, 4),
+                       "measured": f"mean over the {cn4} forward launches of this shape of a C4 training step, "
+                                   "re-issued back to back between HIP events (as the C2 roofline)"},
+          "train_tflops": round(3 * FWD_GFLOP_PER_IMG * args.batch / ms, 2), "sample": {}}
     for w in (0.0, 1.0, 3.0):
         sms, S = sample_rate(model, T, args.sample_batch, w, args.extra_sample_steps, 0, barrier)
         _progress(f"C4 sample w={w:g} {sms:.3f} ms/step")

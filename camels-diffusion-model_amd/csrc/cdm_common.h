@@ -74,3 +74,11 @@ static __device__ __forceinline__ float bn_bwd_elem(float g, float y, float s, f
     const float xh = (y - mean) * invstd;
     return fmaf(cc, xh, fmaf(a, zp > 0.f ? g : 0.f, b));
 }
+
+// XCD-aware block order: consecutive hardware block ids go round-robin over the 8 XCDs (each with its own L2);
+// this returns a logical index such that XCD x owns one contiguous range of logical blocks, so neighbouring work
+// items (e.g. image bands sharing halo rows) run on one XCD and meet in its L2.  A bijection on [0, gridDim.x).
+static __device__ __forceinline__ int xcd_logical_block() {
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+}

@@ -811,6 +811,21 @@ struct PreBnRelu {
     const float* p[2];         // per input channel: scale s, shift t
 };
 static __device__ __forceinline__ float bn_relu_elem(float y, float s, float t) { return relu_f(fmaf(y, s, t)); }
+// PreBnReluSums (kernel-row weight gradient only): the X operand as PreBnRelu, and in addition the producer layer's
+// BatchNorm-backward channel sums, accumulated while its pre-norm output y is staged anyway: with g = the gradient wrt
+// relu(y s + t) (this conv's input, already written by this layer's dgrad), g_pre = (y s + t > 0 ? g : 0) and
+// xhat = (y - mean) invstd:  S1 = sum g_pre, S2 = sum g_pre xhat, S5 = sum xhat per channel (the mode-0 sums of
+// cdm_norm_bwd_reduce, whose pass over g and y this replaces).  Each X pixel is staged by the 3 kernel-row blocks x
+// the co tiles of its split and summed by exactly one of them (spread evenly, see the kernel); one partial per block,
+// sums[(split * 3 + ky) * gx + co tile][5][Cin] (rows 2, 3 zero).
+struct PreBnReluSums {
+    static constexpr bool on = false;
+    static constexpr int kind = 3;
+    const float* p[2];         // per input channel: scale s, shift t
+    const float* g; int ldg;   // grad wrt this conv's input relu(y s + t)
+    const float* mean; const float* invstd;
+    float* sums;
+};
 
 
 // ============================== LDS-halo conv3x3 on the split-bf16 matrix cores ==============================
@@ -1399,7 +1414,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
     constexpr int RA = 16 * KS, RB = RA + 2;          // image rows (pixels): dY, X with its halo
     constexpr int IA = RA * 128, IB = RB * 128;       // bf16 per term image
     constexpr int STEP = NS * (IA + IB);
-    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STEP];
+    // the PreBnReluSums fold reuses the staging buffers as [16 rows][3][128] floats: at least 12288 bf16 of them
+    // (one bf16 term with 16-pixel K steps stages only 8704)
+    constexpr int SMEM = (PX::kind == 3 && 2 * STEP < 2 * 16 * 3 * 128) ? 2 * 16 * 3 * 128 : 2 * STEP;
+    __shared__ __attribute__((aligned(16))) __bf16 smem[SMEM];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
     const int gx = Cout / 128, T = gx * 3 * (Cin / 128);
@@ -1429,9 +1447,23 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
     float4 ra[KS], rb[KS], rb1 = f4zero();
     bool vb[KS], vb1 = false;       // PX: which X pieces lie inside the image (padding stays zero)
     float xs[4], xt[4];             // PX coefficients of this thread's 4 input channels ci0 + c4
-    if constexpr (PX::kind == 2) {
+    if constexpr (PX::kind >= 2) {
         const float4 a = ld4(px.p[0] + ci0 + c4), b = ld4(px.p[1] + ci0 + c4);
         xs[0] = a.x; xs[1] = a.y; xs[2] = a.z; xs[3] = a.w; xt[0] = b.x; xt[1] = b.y; xt[2] = b.z; xt[3] = b.w;
+    }
+    // PreBnReluSums: every X pixel (image row hh, column c) of this ci tile is staged by all 3 x gx blocks of the
+    // split holding its output pixel(s); it is summed by exactly one of them, spread evenly: the kernel-row block
+    // ky = hh % 3 (ky = 1 for the last image row, where hh % 3 == 0 stages no output row) and, per K step q
+    // (global RA-pixel step), the co tile q % gx.  The flag is per K step (block-uniform), set by gload.
+    constexpr bool SUMS = PX::kind == 3;
+    bool sum_step = false;
+    float xm[4], xi[4], s1[4], s2[4], s5[4];
+    float4 gr[SUMS ? KS : 1], gr1 = f4zero();
+    if constexpr (SUMS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { s1[e] = 0.f; s2[e] = 0.f; s5[e] = 0.f; }
+        const float4 a = ld4(px.mean + ci0 + c4), b = ld4(px.invstd + ci0 + c4);
+        xm[0] = a.x; xm[1] = a.y; xm[2] = a.z; xm[3] = a.w; xi[0] = b.x; xi[1] = b.y; xi[2] = b.z; xi[3] = b.w;
     }
     float4 ya[PRE::on ? KS : 1];
     float cf[PRE::on ? 7 : 1][4];   // PreBnBwd coefficients of this thread's 4 output channels m0 + c4
@@ -1446,6 +1478,11 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
         const int hh = ph + ky - 1;
         const bool rowok = (unsigned)hh < (unsigned)H;
         const long long xrow = (long long)(pn * H + hh) * W;
+        if constexpr (SUMS) {
+            const int ks = (hh == H - 1 && hh % 3 == 0) ? 1 : hh % 3;
+            const long long q = ((long long)(pn * H + ph) * W + pw) / RA;
+            sum_step = rowok && ky == ks && (int)(q % gx) == (m0 >> 7);
+        }
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
             const long long pix = (long long)(pn * H + ph) * W + pw + sr + 16 * k;
@@ -1454,17 +1491,33 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
             const int w0 = pw - 1 + sr + 16 * k;
             vb[k] = rowok && (unsigned)w0 < (unsigned)W;
             rb[k] = vb[k] ? ld4(x + (xrow + w0) * ldx + ci0 + c4) : f4zero();
+            if constexpr (SUMS) {   // central rows 1..RA of the X image (the step's own columns, inside the image)
+                gr[k] = (sum_step && (k > 0 || sr >= 1)) ? ld4(px.g + (xrow + w0) * px.ldg + ci0 + c4) : f4zero();
+            }
         }
         if (tid < 64) {
             const int w1 = pw + RA - 1 + sr;
             vb1 = rowok && w1 < W;
             rb1 = vb1 ? ld4(x + (xrow + w1) * ldx + ci0 + c4) : f4zero();
+            if constexpr (SUMS) gr1 = (sum_step && tid < 32) ? ld4(px.g + (xrow + w1) * px.ldg + ci0 + c4) : f4zero();
         }
         pw += RA;
         if (pw >= W) { pw = 0; if (++ph == H) { ph = 0; ++pn; } }
     };
+    auto xsum = [&](const float4& v, const float4& gv) {     // PreBnReluSums: one central piece
+        if constexpr (SUMS) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float y = f4get(v, e);
+                const float zp = fmaf(y, xs[e], xt[e]);
+                const float xh = (y - xm[e]) * xi[e];
+                const float gp = zp > 0.f ? f4get(gv, e) : 0.f;
+                s1[e] += gp; s2[e] += gp * xh; s5[e] += xh;
+            }
+        }
+    };
     auto xpre = [&](const float4& v, bool valid) -> float4 {   // PX transform at staging time (after the load wait)
-        if constexpr (PX::kind == 2) {
+        if constexpr (PX::kind >= 2) {
             if (valid)
                 return make_float4(bn_relu_elem(v.x, xs[0], xt[0]), bn_relu_elem(v.y, xs[1], xt[1]),
                                    bn_relu_elem(v.z, xs[2], xt[2]), bn_relu_elem(v.w, xs[3], xt[3]));
@@ -1496,7 +1549,13 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
             } else {
                 put(a, sr + 16 * k, ra[k], sa, IA);
             }
+            if constexpr (SUMS) {
+                if (sum_step && (k > 0 || sr >= 1)) xsum(rb[k], gr[k]);
+            }
             put(b, sr + 16 * k, xpre(rb[k], vb[k]), sb, IB);
+        }
+        if constexpr (SUMS) {
+            if (sum_step && tid < 32) xsum(rb1, gr1);
         }
         if (tid < 64) put(b, RA + sr, xpre(rb1, vb1), sb, IB);
     };
@@ -1564,6 +1623,25 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
         if (more) sstore(smem + (cur ^ 1) * STEP);
         __syncthreads();
         cur ^= 1;
+    }
+    if constexpr (SUMS) {   // fold the 16 pixel rows of each channel quad (fixed order): one partial per block,
+        float* red = reinterpret_cast<float*>(smem);        // [16 rows][3][128 ch] in the idle staging buffers
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            red[(sr * 3 + 0) * 128 + c4 + e] = s1[e];
+            red[(sr * 3 + 1) * 128 + c4 + e] = s2[e];
+            red[(sr * 3 + 2) * 128 + c4 + e] = s5[e];
+        }
+        __syncthreads();
+        if (tid < 128) {   // sums[(split * 3 + ky) * gx + co tile][5][Cin]
+            float a1 = 0.f, a2 = 0.f, a5 = 0.f;
+            for (int r = 0; r < 16; ++r) {
+                a1 += red[(r * 3 + 0) * 128 + tid]; a2 += red[(r * 3 + 1) * 128 + tid];
+                a5 += red[(r * 3 + 2) * 128 + tid];
+            }
+            float* o = px.sums + ((long long)(bz * 3 + ky) * gx + (m0 >> 7)) * 5 * Cin + ci0 + tid;
+            o[0] = a1; o[Cin] = a2; o[2 * Cin] = 0.f; o[3 * Cin] = 0.f; o[4 * Cin] = a5;
+        }
     }
     float ia = 1.f, ib = 1.f;
     if constexpr (NT == NT_H3) { ia = 1.f / sa; ib = 1.f / sb; }
@@ -1965,23 +2043,38 @@ CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int C
     return cdm_status();
 }
 
+// The "x16" entry points below run the LDS-halo / kernel-row / split-GEMM kernels in either 16-bit arithmetic
+// (nterm = NT_H3: fp32-class scaled fp16 hi/lo; nterm = 1: one bf16 term, the C4 mixed-precision configuration),
+// with every train-mode fusion available to both; the *_h3 names are the same calls with nterm = NT_H3.  The operand
+// maxima (amax_*) scale the h3 operands only and may be null for nterm = 1.
+static bool x16_ok(int nterm) { return nterm == NT_H3 || nterm == 1; }
+static bool x16_amax_ok(int nterm, const void* a, const void* b) { return nterm != NT_H3 || (a && b); }
+
 // conv3x3 dgrad of a Conv -> BatchNorm -> ReLU layer with the BN backward fused into the halo staging: the conv
 // input dy = bn_bwd_elem(g, y, coefficients) is computed per staged element (dy never materialised).  C = BN
 // channels (the dgrad's input channels), Cout = the dgrad's output channels.  W == H in {32, 64, 128}, C % 16 == 0,
 // C <= 256; wx = cdm_split_f16x2 of the kc = 16 packed dgrad weights; max|dy| <= *amax_dy (cdm_bn_bwd_amax_bound).
-CDM_API int cdm_conv3x3_dgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
-                                       const float* t, const float* mean, const float* invstd, const float* A,
-                                       const float* B, const float* Cc, int N, int H, int W, int C, const void* wx,
-                                       const float* amax_dy, const float* amax_w, float* out, int ldo, int Cout,
-                                       int flags, float* amax_out, void* stream) {
-    if (W != H || !halo_width_ok(W, NT_H3) || W > 128 || C % 16 || C > 256 || ldg % 4 || ldy % 4 || (H * W) % HBM_ ||
-        !amax_dy || !amax_w)
+CDM_API int cdm_conv3x3_dgrad_x16_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
+                                        const float* t, const float* mean, const float* invstd, const float* A,
+                                        const float* B, const float* Cc, int N, int H, int W, int C, const void* wx,
+                                        const float* amax_dy, const float* amax_w, float* out, int ldo, int Cout,
+                                        int flags, float* amax_out, int nterm, void* stream) {
+    if (!x16_ok(nterm) || W != H || !halo_width_ok(W, nterm) || W > 128 || C % 16 || C > 256 || ldg % 4 || ldy % 4 ||
+        (H * W) % HBM_ || !x16_amax_ok(nterm, amax_dy, amax_w))
         return (int)hipErrorInvalidValue;
     const int M = N * H * W;
     const EpiStoreW<4> eh{out, ldo, 0, nullptr, Cout, flags, nullptr, 0, M, Cout, amax_out};
     const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
     const __bf16* b = reinterpret_cast<const __bf16*>(wx);
-    return launch_conv_halo_w(W, g, N, H, C, ldg, b, Cout, amax_dy, amax_w, eh, NT_H3, S(stream), pre);
+    return launch_conv_halo_w(W, g, N, H, C, ldg, b, Cout, amax_dy, amax_w, eh, nterm, S(stream), pre);
+}
+CDM_API int cdm_conv3x3_dgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
+                                       const float* t, const float* mean, const float* invstd, const float* A,
+                                       const float* B, const float* Cc, int N, int H, int W, int C, const void* wx,
+                                       const float* amax_dy, const float* amax_w, float* out, int ldo, int Cout,
+                                       int flags, float* amax_out, void* stream) {
+    return cdm_conv3x3_dgrad_x16_bnbwd(g, ldg, y, ldy, s, t, mean, invstd, A, B, Cc, N, H, W, C, wx, amax_dy, amax_w,
+                                       out, ldo, Cout, flags, amax_out, NT_H3, stream);
 }
 
 CDM_API int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx3,
@@ -1992,12 +2085,19 @@ CDM_API int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int
                              nterm, nullptr, S(stream));
 }
 
+CDM_API int cdm_conv3x3_fwd_x16(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx,
+                                const float* amax_x, const float* amax_w, const float* bias, float* y, int ldy,
+                                int Cout, int flags, float* stats, int stats_ld, int kc, float* amax_y, int nterm,
+                                void* stream) {
+    if (!x16_ok(nterm) || !x16_amax_ok(nterm, amax_x, amax_w)) return (int)hipErrorInvalidValue;
+    return conv3x3_fwd_split(x, N, H, W, Cin, ldx, wx, amax_x, amax_w, bias, y, ldy, Cout, flags, stats, stats_ld, kc,
+                             nterm, amax_y, S(stream));
+}
 CDM_API int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
                                const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags,
                                float* stats, int stats_ld, int kc, float* amax_y, void* stream) {
-    if (!amax_x || !amax_w) return (int)hipErrorInvalidValue;
-    return conv3x3_fwd_split(x, N, H, W, Cin, ldx, wx, amax_x, amax_w, bias, y, ldy, Cout, flags, stats, stats_ld, kc,
-                             NT_H3, amax_y, S(stream));
+    return cdm_conv3x3_fwd_x16(x, N, H, W, Cin, ldx, wx, amax_x, amax_w, bias, y, ldy, Cout, flags, stats, stats_ld, kc,
+                               amax_y, NT_H3, stream);
 }
 
 // cdm_conv3x3_fwd_h3 + two fusions of the train-mode Conv -> BatchNorm -> ReLU chain (LDS-halo path only):
@@ -2005,13 +2105,20 @@ CDM_API int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int
 //                             (its BN apply runs in this conv's staging; *amax_x must bound that z)
 //   ymm (optional, needs stats): per output channel max / min of y as ordered-int keys, ymm[c] / ymm[ymm_ld + c]
 //                             (cleared by the caller to INT_MIN / INT_MAX), for the next layer's exact max|z|
+CDM_API int cdm_conv3x3_fwd_x16_ex(const float* x, int N, int H, int W, int Cin, int ldx, const float* pre_s,
+                                   const float* pre_t, const void* wx, const float* amax_x, const float* amax_w,
+                                   const float* bias, float* y, int ldy, int Cout, int flags, float* stats,
+                                   int stats_ld, int kc, float* amax_y, int* ymm, int ymm_ld, int nterm, void* stream) {
+    if (!x16_ok(nterm) || !x16_amax_ok(nterm, amax_x, amax_w)) return (int)hipErrorInvalidValue;
+    return conv3x3_fwd_split(x, N, H, W, Cin, ldx, wx, amax_x, amax_w, bias, y, ldy, Cout, flags, stats, stats_ld, kc,
+                             nterm, amax_y, S(stream), pre_s, pre_t, ymm, ymm_ld);
+}
 CDM_API int cdm_conv3x3_fwd_h3_ex(const float* x, int N, int H, int W, int Cin, int ldx, const float* pre_s,
                                   const float* pre_t, const void* wx, const float* amax_x, const float* amax_w,
                                   const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
                                   int kc, float* amax_y, int* ymm, int ymm_ld, void* stream) {
-    if (!amax_x || !amax_w) return (int)hipErrorInvalidValue;
-    return conv3x3_fwd_split(x, N, H, W, Cin, ldx, wx, amax_x, amax_w, bias, y, ldy, Cout, flags, stats, stats_ld, kc,
-                             NT_H3, amax_y, S(stream), pre_s, pre_t, ymm, ymm_ld);
+    return cdm_conv3x3_fwd_x16_ex(x, N, H, W, Cin, ldx, pre_s, pre_t, wx, amax_x, amax_w, bias, y, ldy, Cout, flags,
+                                  stats, stats_ld, kc, amax_y, ymm, ymm_ld, NT_H3, stream);
 }
 
 template <int KS, class PRE = PreNone, class PX = PreNone>
@@ -2020,10 +2127,21 @@ static int launch_wgrad_row(const float* dy, int lddy, int Cout, const float* x,
                             PRE pre = PRE{}, PX px = PX{}) {
     const int ktiles = K / (16 * KS), per = (ktiles + sp - 1) / sp;
     dim3 grid((Cout / 128) * 3 * (Cin / 128) * ((ktiles + per - 1) / per));
-    if constexpr (PX::kind != 0) {            // the fused X transform is instantiated for the h3 arithmetic only
-        if (nterm != NT_H3) return (int)hipErrorInvalidValue;
-        hipLaunchKernelGGL((wgrad3x3_row_kernel<NT_H3, KS, PRE, PX>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W,
-                           Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px);
+    if constexpr (KS == 4) {   // 64-pixel K steps: the one-term bf16 images only (66 KiB of LDS; h3 would need 133)
+        if (nterm != 1) return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL((wgrad3x3_row_kernel<1, 4, PRE, PX>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin,
+                           ldx, ktiles, per, amax_dy, amax_x, slab, pre, px);
+        return cdm_status();
+    } else {
+    if constexpr (PX::kind != 0) {            // the fused X transform: the 16-bit arithmetics (h3, bf16)
+        if (nterm == NT_H3)
+            hipLaunchKernelGGL((wgrad3x3_row_kernel<NT_H3, KS, PRE, PX>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H,
+                               W, Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px);
+        else if (nterm == 1)
+            hipLaunchKernelGGL((wgrad3x3_row_kernel<1, KS, PRE, PX>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W,
+                               Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px);
+        else
+            return (int)hipErrorInvalidValue;
         return cdm_status();
     }
     switch (nterm) {
@@ -2038,6 +2156,7 @@ static int launch_wgrad_row(const float* dy, int lddy, int Cout, const float* x,
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();
+    }
 }
 
 // conv3x3 weight gradient on the 16-bit matrix cores (same slab contract as cdm_conv3x3_wgrad); W % 8 == 0
@@ -2083,11 +2202,16 @@ CDM_API int cdm_conv3x3_wgrad_x3(const float* dy, int lddy, int Cout, const floa
     return conv3x3_wgrad_split(dy, lddy, Cout, x, N, H, W, Cin, ldx, nullptr, nullptr, splits, slab, nterm, S(stream));
 }
 
+CDM_API int cdm_conv3x3_wgrad_x16(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,
+                                  int ldx, const float* amax_dy, const float* amax_x, int splits, float* slab, int nterm,
+                                  void* stream) {
+    if (!x16_ok(nterm) || !x16_amax_ok(nterm, amax_dy, amax_x)) return (int)hipErrorInvalidValue;
+    return conv3x3_wgrad_split(dy, lddy, Cout, x, N, H, W, Cin, ldx, amax_dy, amax_x, splits, slab, nterm, S(stream));
+}
 CDM_API int cdm_conv3x3_wgrad_h3(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,
                                  int ldx, const float* amax_dy, const float* amax_x, int splits, float* slab,
                                  void* stream) {
-    if (!amax_dy || !amax_x) return (int)hipErrorInvalidValue;
-    return conv3x3_wgrad_split(dy, lddy, Cout, x, N, H, W, Cin, ldx, amax_dy, amax_x, splits, slab, NT_H3, S(stream));
+    return cdm_conv3x3_wgrad_x16(dy, lddy, Cout, x, N, H, W, Cin, ldx, amax_dy, amax_x, splits, slab, NT_H3, stream);
 }
 
 // measurement entry: variant 0 = kernel-row kernel, 32-pixel K steps (default path), 1 = per-tap kernel,
@@ -2102,46 +2226,76 @@ CDM_API int cdm_conv3x3_wgrad_h3_variant(const float* dy, int lddy, int Cout, co
 
 // conv3x3 weight gradient of a Conv -> BatchNorm -> ReLU layer with the BN backward fused into the dY staging of
 // the kernel-row kernel (same slab contract as cdm_conv3x3_wgrad_h3).  Cin % 128 == Cout % 128 == 0, W % 16 == 0.
+CDM_API int cdm_conv3x3_wgrad_x16_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
+                                        const float* t, const float* mean, const float* invstd, const float* A,
+                                        const float* B, const float* Cc, int Cout, const float* x, int N, int H, int W,
+                                        int Cin, int ldx, const float* amax_dy, const float* amax_x, int splits,
+                                        float* slab, int nterm, void* stream) {
+    if (!x16_ok(nterm) || Cin % 128 || Cout % 128 || W % 16 || ldg % 4 || ldy % 4 || ldx % 4 ||
+        !x16_amax_ok(nterm, amax_dy, amax_x))
+        return (int)hipErrorInvalidValue;
+    const int K = N * H * W, sp = effective_splits(K, splits);
+    const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
+    if (W % 32 == 0 && effective_splits(K, splits, 32) == sp)
+        return launch_wgrad_row<2>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, nterm, S(stream), pre);
+    if (effective_splits(K, splits, 16) == sp)
+        return launch_wgrad_row<1>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, nterm, S(stream), pre);
+    return (int)hipErrorInvalidValue;
+}
 CDM_API int cdm_conv3x3_wgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
                                        const float* t, const float* mean, const float* invstd, const float* A,
                                        const float* B, const float* Cc, int Cout, const float* x, int N, int H, int W,
                                        int Cin, int ldx, const float* amax_dy, const float* amax_x, int splits,
                                        float* slab, void* stream) {
-    if (Cin % 128 || Cout % 128 || W % 16 || ldg % 4 || ldy % 4 || ldx % 4 || !amax_dy || !amax_x)
-        return (int)hipErrorInvalidValue;
-    const int K = N * H * W, sp = effective_splits(K, splits);
-    const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
-    if (W % 32 == 0 && effective_splits(K, splits, 32) == sp)
-        return launch_wgrad_row<2>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, NT_H3, S(stream), pre);
-    if (effective_splits(K, splits, 16) == sp)
-        return launch_wgrad_row<1>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, NT_H3, S(stream), pre);
-    return (int)hipErrorInvalidValue;
+    return cdm_conv3x3_wgrad_x16_bnbwd(g, ldg, y, ldy, s, t, mean, invstd, A, B, Cc, Cout, x, N, H, W, Cin, ldx, amax_dy,
+                                       amax_x, splits, slab, NT_H3, stream);
 }
 
 // the kernel-row weight gradient with both staging fusions selectable: g / y / BN coefficients (optional, all or
 // none: the dY operand is the BN backward of g, as cdm_conv3x3_wgrad_h3_bnbwd) and x_s / x_t (optional: the X operand
 // is relu(x * x_s[c] + x_t[c]) of the previous layer's pre-norm output).  Cin % 128 == Cout % 128 == 0, W % 16 == 0.
+CDM_API int cdm_conv3x3_wgrad_x16_ex(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
+                                     const float* mean, const float* invstd, const float* A, const float* B,
+                                     const float* Cc, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,
+                                     const float* x_s, const float* x_t, const float* x_g, int ldxg,
+                                     const float* x_mean, const float* x_invstd, float* x_sums,
+                                     const float* amax_dy, const float* amax_x, int splits, float* slab, int nterm,
+                                     void* stream) {
+    if (!x16_ok(nterm) || Cin % 128 || Cout % 128 || W % 16 || ldg % 4 || ldx % 4 ||
+        !x16_amax_ok(nterm, amax_dy, amax_x) || (x_s && !x_t) || (y && ldy % 4) ||
+        (x_sums && (!x_s || !x_g || ldxg % 4 || !x_mean || !x_invstd)))
+        return (int)hipErrorInvalidValue;
+    const int K = N * H * W, sp = effective_splits(K, splits);
+    const bool ks2 = W % 32 == 0 && effective_splits(K, splits, 32) == sp;
+    // (64-pixel K steps for the one-term bf16 images measured 1.81x slower per launch than 32: 1284 vs 710 us on the
+    // C4 step's 128 -> 128 @64^2 weight gradients, profiles/r3_c4_ks4.txt — not used)
+    const bool ks4 = false;
+    if (!ks2 && effective_splits(K, splits, 16) != sp) return (int)hipErrorInvalidValue;
+    const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
+    const PreBnRelu px{{x_s, x_t}};
+    const PreBnReluSums pxs{{x_s, x_t}, x_g, ldxg, x_mean, x_invstd, x_sums};
+    hipStream_t st = S(stream);
+#define CDM_WG(KS_, PRE_, PX_) launch_wgrad_row<KS_>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, \
+                                                     nterm, st, PRE_, PX_)
+#define CDM_WGK(PRE_, PX_) (ks4 ? CDM_WG(4, PRE_, PX_) : ks2 ? CDM_WG(2, PRE_, PX_) : CDM_WG(1, PRE_, PX_))
+    if (x_sums) {   // the producer's BN-backward sums ride along (x_sums[splits][5][Cin])
+        if (y) return CDM_WGK(pre, pxs);
+        return CDM_WGK(PreNone{}, pxs);
+    }
+    if (y && x_s) return CDM_WGK(pre, px);
+    if (y) return CDM_WGK(pre, PreNone{});
+    if (x_s) return CDM_WGK(PreNone{}, px);
+    return CDM_WGK(PreNone{}, PreNone{});
+#undef CDM_WGK
+#undef CDM_WG
+}
 CDM_API int cdm_conv3x3_wgrad_h3_ex(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
                                     const float* mean, const float* invstd, const float* A, const float* B,
                                     const float* Cc, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,
                                     const float* x_s, const float* x_t, const float* amax_dy, const float* amax_x,
                                     int splits, float* slab, void* stream) {
-    if (Cin % 128 || Cout % 128 || W % 16 || ldg % 4 || ldx % 4 || !amax_dy || !amax_x || (x_s && !x_t) ||
-        (y && ldy % 4))
-        return (int)hipErrorInvalidValue;
-    const int K = N * H * W, sp = effective_splits(K, splits);
-    const bool ks2 = W % 32 == 0 && effective_splits(K, splits, 32) == sp;
-    if (!ks2 && effective_splits(K, splits, 16) != sp) return (int)hipErrorInvalidValue;
-    const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
-    const PreBnRelu px{{x_s, x_t}};
-    hipStream_t st = S(stream);
-#define CDM_WG(KS_, PRE_, PX_) launch_wgrad_row<KS_>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, \
-                                                     NT_H3, st, PRE_, PX_)
-    if (y && x_s) return ks2 ? CDM_WG(2, pre, px) : CDM_WG(1, pre, px);
-    if (y) return ks2 ? CDM_WG(2, pre, PreNone{}) : CDM_WG(1, pre, PreNone{});
-    if (x_s) return ks2 ? CDM_WG(2, PreNone{}, px) : CDM_WG(1, PreNone{}, px);
-    return ks2 ? CDM_WG(2, PreNone{}, PreNone{}) : CDM_WG(1, PreNone{}, PreNone{});
-#undef CDM_WG
+    return cdm_conv3x3_wgrad_x16_ex(g, ldg, y, ldy, s, t, mean, invstd, A, B, Cc, Cout, x, N, H, W, Cin, ldx, x_s, x_t,
+                                    nullptr, 0, nullptr, nullptr, nullptr, amax_dy, amax_x, splits, slab, NT_H3, stream);
 }
 
 static int split_blocks(int K, int N) {
@@ -2222,15 +2376,20 @@ CDM_API int cdm_convT2x2_fwd(const float* x, int N, int H, int W, int Cin, int l
 }
 
 // the same on the fp16 matrix cores (h3: scaled hi/lo split, see split_terms); wx = cdm_split_f16x2 of wpk
-CDM_API int cdm_convT2x2_fwd_h3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx,
-                                const float* amax_x, const float* amax_w, const float* bias, float* y, int ldy,
-                                int Cout, float* amax_y, void* stream) {
-    if (Cin % 4 || Cout % 4 || !amax_x || !amax_w) return (int)hipErrorInvalidValue;
+CDM_API int cdm_convT2x2_fwd_x16(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx,
+                                 const float* amax_x, const float* amax_w, const float* bias, float* y, int ldy,
+                                 int Cout, float* amax_y, int nterm, void* stream) {
+    if (!x16_ok(nterm) || Cin % 4 || Cout % 4 || !x16_amax_ok(nterm, amax_x, amax_w)) return (int)hipErrorInvalidValue;
     const int M = N * H * W, K = Cin, NN = 4 * Cout;
     EpiConvT2x2 ep{y, ldy, bias, H, W, Cout, M, NN, amax_y};
     return launch_gemm_x3<RowK<LdDenseA>::template T, StagePre, EpiConvT2x2, true>(
         MkRowK<LdDenseA>{LdDenseA{x, ldx, M, K}, amax_x}, MkPre{reinterpret_cast<const __bf16*>(wx), NN, amax_w}, ep,
-        M, NN, K, 1, NT_H3, S(stream));
+        M, NN, K, 1, nterm, S(stream));
+}
+CDM_API int cdm_convT2x2_fwd_h3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx,
+                                const float* amax_x, const float* amax_w, const float* bias, float* y, int ldy,
+                                int Cout, float* amax_y, void* stream) {
+    return cdm_convT2x2_fwd_x16(x, N, H, W, Cin, ldx, wx, amax_x, amax_w, bias, y, ldy, Cout, amax_y, NT_H3, stream);
 }
 
 // dX[n,h,w,ci] (+)= sum_{ij,co} dY[n,2h+i,2w+j,co] * W[ci][co][ij];  H, W are the INPUT (small) grid
@@ -2246,29 +2405,40 @@ CDM_API int cdm_convT2x2_dgrad(const float* dy, int N, int H, int W, int Cout, i
 
 // h3 ConvT 2x2 dgrad: A = gathered dY (k = (ij, co), max|dY| = *amax_dy), B = cdm_split_f16x2 of the packed
 // wpkT [4 Cout][Cin] with max|W| = *amax_w
-CDM_API int cdm_convT2x2_dgrad_h3(const float* dy, int N, int H, int W, int Cout, int lddy, const void* wx,
-                                  const float* amax_dy, const float* amax_w, float* dx, int lddx, int Cin, int flags,
-                                  void* stream) {
-    if (Cin % 4 || Cout % 4 || !amax_dy || !amax_w) return (int)hipErrorInvalidValue;
+CDM_API int cdm_convT2x2_dgrad_x16(const float* dy, int N, int H, int W, int Cout, int lddy, const void* wx,
+                                   const float* amax_dy, const float* amax_w, float* dx, int lddx, int Cin, int flags,
+                                   int nterm, void* stream) {
+    if (!x16_ok(nterm) || Cin % 4 || Cout % 4 || !x16_amax_ok(nterm, amax_dy, amax_w)) return (int)hipErrorInvalidValue;
     const int M = N * H * W, K = 4 * Cout;
     EpiStore ep{dx, lddx, 0, nullptr, 1, flags, nullptr, 0, M, Cin};
     return launch_gemm_x3<RowK<LdConvT2x2GatherA>::template T, StagePre, EpiStore, true>(
         MkRowK<LdConvT2x2GatherA>{LdConvT2x2GatherA{dy, H, W, Cout, lddy, M, K}, amax_dy},
-        MkPre{reinterpret_cast<const __bf16*>(wx), Cin, amax_w}, ep, M, Cin, K, 1, NT_H3, S(stream));
+        MkPre{reinterpret_cast<const __bf16*>(wx), Cin, amax_w}, ep, M, Cin, K, 1, nterm, S(stream));
+}
+CDM_API int cdm_convT2x2_dgrad_h3(const float* dy, int N, int H, int W, int Cout, int lddy, const void* wx,
+                                  const float* amax_dy, const float* amax_w, float* dx, int lddx, int Cin, int flags,
+                                  void* stream) {
+    return cdm_convT2x2_dgrad_x16(dy, N, H, W, Cout, lddy, wx, amax_dy, amax_w, dx, lddx, Cin, flags, NT_H3, stream);
 }
 
 // h3 ConvT 2x2 weight gradient (same slab contract as cdm_convT2x2_wgrad); W % 8 == 0
-CDM_API int cdm_convT2x2_wgrad_h3(const float* x, int N, int H, int W, int Cin, int ldx, const float* dy, int Cout,
-                                  int lddy, const float* amax_x, const float* amax_dy, int splits, float* slab,
-                                  void* stream) {
-    if (Cin % 4 || Cout % 4 || W % 8 || !amax_x || !amax_dy) return (int)hipErrorInvalidValue;
+CDM_API int cdm_convT2x2_wgrad_x16(const float* x, int N, int H, int W, int Cin, int ldx, const float* dy, int Cout,
+                                   int lddy, const float* amax_x, const float* amax_dy, int splits, float* slab,
+                                   int nterm, void* stream) {
+    if (!x16_ok(nterm) || Cin % 4 || Cout % 4 || W % 8 || !x16_amax_ok(nterm, amax_x, amax_dy))
+        return (int)hipErrorInvalidValue;
     const int M = Cin, NN = 4 * Cout, K = N * H * W;
     const int sp = effective_splits(K, splits);
     EpiStore ep{slab, NN, (long long)M * NN, nullptr, 1, 0, nullptr, 0, M, NN};
     return launch_gemm_x3<ColK<LdDenseAT>::template T, ColK<LdConvT2x2GatherB>::template T, EpiStore, false>(
         MkColK<LdDenseAT>{LdDenseAT{x, ldx, M, K}, amax_x},
-        MkColK<LdConvT2x2GatherB>{LdConvT2x2GatherB{dy, H, W, Cout, lddy, K, NN}, amax_dy}, ep, M, NN, K, sp, NT_H3,
+        MkColK<LdConvT2x2GatherB>{LdConvT2x2GatherB{dy, H, W, Cout, lddy, K, NN}, amax_dy}, ep, M, NN, K, sp, nterm,
         S(stream));
+}
+CDM_API int cdm_convT2x2_wgrad_h3(const float* x, int N, int H, int W, int Cin, int ldx, const float* dy, int Cout,
+                                  int lddy, const float* amax_x, const float* amax_dy, int splits, float* slab,
+                                  void* stream) {
+    return cdm_convT2x2_wgrad_x16(x, N, H, W, Cin, ldx, dy, Cout, lddy, amax_x, amax_dy, splits, slab, NT_H3, stream);
 }
 
 // C[m][n] = A[m][k] . B[k][n] (+bias[n % bias_mod]).  splits > 1: writes raw partials to slab[z][M][N].

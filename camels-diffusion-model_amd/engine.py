@@ -115,11 +115,18 @@ class UNetEngine:
         self.nf, self.ncf, self.H = n_feat, n_cfeat, height
         self.conv_math = conv_math
         self.nterm = CONV_MATH[conv_math]
-        # h3 train: BatchNorm backward fused into the staging of the layer's dgrad / wgrad (dy never written);
+        # the 16-bit-MFMA kernel family with every train-mode fusion: h3 (fp32-class) and bf16 (C4 mixed precision)
+        self.x16 = self.nterm in (1, NT_H3)
+        self.h3 = self.nterm == NT_H3
+        # BatchNorm backward fused into the staging of the layer's dgrad / wgrad (dy never written);
         # $CDM_FUSE_BN_BWD=0 keeps the separate apply kernel (A/B checks)
-        self.fuse_bn_bwd = self.nterm == NT_H3 and os.environ.get("CDM_FUSE_BN_BWD", "1") != "0"
-        # h3 train: a dense BatchNorm + ReLU applied inside the next conv's staging ($CDM_FUSE_BN_FWD=0: apply kernel)
-        self.fuse_bn_fwd = self.nterm == NT_H3 and os.environ.get("CDM_FUSE_BN_FWD", "1") != "0"
+        self.fuse_bn_bwd = self.x16 and os.environ.get("CDM_FUSE_BN_BWD", "1") != "0"
+        # a dense BatchNorm + ReLU applied inside the next conv's staging ($CDM_FUSE_BN_FWD=0: apply kernel)
+        self.fuse_bn_fwd = self.x16 and os.environ.get("CDM_FUSE_BN_FWD", "1") != "0"
+        # a fused producer's BN-backward channel sums accumulated in its consumer's weight-gradient X staging (which
+        # stages the producer's y anyway), after the consumer's dgrad wrote the producer's g: no separate pass over g and
+        # y ($CDM_FUSE_BN_SUMS=0: cdm_norm_bwd_reduce)
+        self.fuse_bn_sums = self.x16 and os.environ.get("CDM_FUSE_BN_SUMS", "1") != "0"
         # init_conv.conv1's BN backward inside its weight-gradient kernel ($CDM_FUSE_CIN1_BWD=0: the apply kernel)
         self.fuse_cin1_bwd = os.environ.get("CDM_FUSE_CIN1_BWD", "1") != "0"
         self.device = torch.device(device)
@@ -224,7 +231,7 @@ class UNetEngine:
             wtT = self._buf(name + ".wtT", (4 * nf, cin))
             lb.cdm_pack_convT(_p(P[name + ".weight"]), cin, nf, 4, _p(wt), _p(wtT) if train else None, stream)
             self.pk[name + ".wt"], self.pk[name + ".wtT"] = wt, wtT
-            if self.nterm == NT_H3:
+            if self.x16:
                 self._split(name + ".wt", cin, 4 * nf, stream)
                 if train:
                     self._split(name + ".wtT", 4 * nf, cin, stream)
@@ -270,6 +277,10 @@ class UNetEngine:
             lib().cdm_split_bf16x3(_p(self.pk[name]), N, K, N, _p(xb), stream)
         self.pk[name + "_x"] = xb
 
+    def _wamax(self, key):
+        """Device max|W| of the split weights pk[key + "_x"] (h3 scale), None for the other arithmetics."""
+        return _p(self.pk[key + "_amax"]) if self.h3 else None
+
     def conv3x3(self, key, x_p, B, S, cin, ldx, bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, s,
                 amax_x=None, amax_y=None, pre=None, ymm=None):
         """3x3 conv (fwd or dgrad) with the packed weights pk[key], in this engine's conv arithmetic.
@@ -286,21 +297,20 @@ class UNetEngine:
 
     def _conv3x3(self, key, x_p, B, S, cin, ldx, bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, s, amax_x,
                  amax_y, pre, ymm):
-        if self.nterm == NT_H3:
-            if amax_x is None:
+        if self.x16:
+            if self.h3 and amax_x is None:
                 assert pre is None
                 amax_x = _p(self._amax)
                 lib().cdm_amax_f32(x_p, B * S * S, cin, ldx, amax_x, 0, s)
             if pre is not None or ymm is not None:
                 ps, pt = pre if pre is not None else (None, None)
                 ym, yld = ymm if ymm is not None else (None, 0)
-                lib().cdm_conv3x3_fwd_h3_ex(x_p, B, S, S, cin, ldx, ps, pt, _p(self.pk[key + "_x"]), amax_x,
-                                            _p(self.pk[key + "_amax"]), bias_p, y_p, ldy, cout, flags, stats_p,
-                                            stats_ld, kc, amax_y, ym, yld, s)
+                lib().cdm_conv3x3_fwd_x16_ex(x_p, B, S, S, cin, ldx, ps, pt, _p(self.pk[key + "_x"]), amax_x,
+                                             self._wamax(key), bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc,
+                                             amax_y, ym, yld, self.nterm, s)
                 return
-            lib().cdm_conv3x3_fwd_h3(x_p, B, S, S, cin, ldx, _p(self.pk[key + "_x"]), amax_x,
-                                     _p(self.pk[key + "_amax"]), bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc,
-                                     amax_y, s)
+            lib().cdm_conv3x3_fwd_x16(x_p, B, S, S, cin, ldx, _p(self.pk[key + "_x"]), amax_x, self._wamax(key),
+                                      bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, amax_y, self.nterm, s)
         elif self.nterm:
             lib().cdm_conv3x3_fwd_x3(x_p, B, S, S, cin, ldx, _p(self.pk[key + "_x"]), bias_p, y_p, ldy, cout, flags,
                                      stats_p, stats_ld, kc, self.nterm, s)
@@ -327,7 +337,8 @@ class UNetEngine:
         if i + 1 >= len(self.layers):
             return False
         c = self.layers[i + 1]
-        halo = lambda L: L.kc == 16 and L.S in (32, 64, 128, 256) and (L.S * L.S) % 256 == 0   # noqa: E731
+        widths = (32, 64, 128, 256) if self.h3 else (32, 64)     # the wide-row LDS-halo conv is h3-only
+        halo = lambda L: L.kc == 16 and L.S in widths and (L.S * L.S) % 256 == 0   # noqa: E731
         # the producer's max / min of y: from its conv epilogue (LDS-halo path), or from the statistics pass of the
         # C_in = 1 init conv (cdm_reduce_stats_mm)
         return ((l.cin == 1 or halo(l)) and halo(c) and c.cin == l.cout and c.cin <= 256 and c.cin % 128 == 0
@@ -335,7 +346,8 @@ class UNetEngine:
 
     def fuses_bn_bwd(self, l: "LayerSpec", kind: str, B: int = 1) -> bool:
         """Layer l's BN backward runs inside its dgrad / wgrad staging (cdm_conv3x3_*_h3_bnbwd)."""
-        return (self.fuse_bn_bwd and kind in ("dense", "plain", "resid") and l.cin > 1 and l.S in (32, 64, 128)
+        return (self.fuse_bn_bwd and kind in ("dense", "plain", "resid") and l.cin > 1
+                and l.S in ((32, 64, 128) if self.h3 else (32, 64))
                 and self.halo_addressable(B, l.S)
                 and l.kc == 16 and l.cin % 128 == 0 and l.cout % 128 == 0 and l.cout <= 256)
 
@@ -388,7 +400,7 @@ class UNetEngine:
         ws.sc_pending = (sc_w, sc_b, sc_split)
         if self.nterm == NT_H3:
             lb.cdm_zero_f32(_p(ws.amax), ws.amax.numel(), s)
-        if train and ws.fused_fwd:
+        if train and ws.fused_fwd and self.h3:
             half = ws.ymm.numel() // 2
             lb.cdm_fill_i32(_p(ws.ymm), half, -2 ** 31, s)               # max keys
             lb.cdm_fill_i32(_p(ws.ymm) + 4 * half, half, 2 ** 31 - 1, s)  # min keys
@@ -458,10 +470,10 @@ class UNetEngine:
     def convT2x2(self, ws, name, x: Act, B, Hin, cin, P, y, src_slot, dst_slot, s):
         """ConvTranspose2d(cin, nf, 2, 2) (diffusion_utilities.py:86) of x [B,Hin,Hin,cin] into y [B,2Hin,2Hin,nf]."""
         nf = self.nf
-        if self.nterm == NT_H3:
-            lib().cdm_convT2x2_fwd_h3(x.p, B, Hin, Hin, cin, x.ld, _p(self.pk[name + ".wt_x"]), self._slot(ws, src_slot),
-                                      _p(self.pk[name + ".wt_amax"]), _p(P[name + ".bias"]), _p(y), nf, nf,
-                                      self._slot(ws, dst_slot), s)
+        if self.x16:
+            lib().cdm_convT2x2_fwd_x16(x.p, B, Hin, Hin, cin, x.ld, _p(self.pk[name + ".wt_x"]),
+                                       self._slot(ws, src_slot), self._wamax(name + ".wt"), _p(P[name + ".bias"]),
+                                       _p(y), nf, nf, self._slot(ws, dst_slot), self.nterm, s)
         else:
             lib().cdm_convT2x2_fwd(x.p, B, Hin, Hin, cin, x.ld, _p(self.pk[name + ".wt"]), _p(P[name + ".bias"]),
                                    _p(y), nf, nf, self._slot(ws, dst_slot), s)
@@ -477,13 +489,13 @@ class UNetEngine:
             if l.cin == 1:
                 lb.cdm_conv3x3_cin1_fwd(_p(x), B, S, S, _p(self.pk[l.name + ".wpk"]), _p(P[l.b]), _p(y), l.cout,
                                         l.cout, 0, None, s)
-                ymm_p, ymm_ld = ws.ymm_of(l) if l.name in ws.fused_fwd else (None, 0)
+                ymm_p, ymm_ld = ws.ymm_of(l) if (l.name in ws.fused_fwd and self.h3) else (None, 0)
                 lb.cdm_reduce_stats_mm(_p(y), l.cout, B, S * S, l.cout, CHUNK, _p(ws.slab), ymm_p, ymm_ld, s)
                 ntiles = B * _cdiv(S * S, CHUNK)
             else:
                 yslot = self._slot(ws, "y:" + l.name) if l.name in ws.fused else None
                 src, pre = self._src_pre(ws, l)
-                ymm = ws.ymm_of(l) if l.name in ws.fused_fwd else None
+                ymm = ws.ymm_of(l) if (l.name in ws.fused_fwd and self.h3) else None
                 self.conv3x3(l.name + ".wpk", src.p, B, S, l.cin, src.ld, _p(P[l.b]), _p(y), l.cout, l.cout, 0,
                              _p(ws.slab), l.cout, l.kc, s, amax_x=self._src_slot(ws, l), amax_y=yslot, pre=pre,
                              ymm=ymm)
@@ -491,7 +503,7 @@ class UNetEngine:
             bn = l.bn
             nparts = fold(ws, _p(ws.slab), ntiles, 2, l.cout, s)
             fused_fwd = l.name in ws.fused_fwd
-            ymm_p, ymm_ld = ws.ymm_of(l) if fused_fwd else (None, 0)
+            ymm_p, ymm_ld = ws.ymm_of(l) if (fused_fwd and self.h3) else (None, 0)
             lb.cdm_bn_fwd_finalize(_p(ws.dpart), nparts, 2, l.cout, float(npix), _p(P[bn + ".weight"]),
                                    _p(P[bn + ".bias"]), _p(P[bn + ".running_mean"]), _p(P[bn + ".running_var"]),
                                    _p(P[bn + ".num_batches_tracked"]), BN_MOM, BN_EPS, _p(st["mean"]),
@@ -672,14 +684,19 @@ class UNetEngine:
             film_a, film_an = ws.emb["contextembed2"], (C if ws.c_rows > 1 else 0)
         HWp = (S // 2) * (S // 2) if mode == 1 else S * S
         nch = _cdiv(HWp, CHUNK)
-        lb.cdm_norm_bwd_reduce(mode, g.p, g.ld, _p(y), C, B, S, S, C, _p(st["scale"]), _p(st["shift"]), 0,
-                               _p(st["mean"]), _p(st["invstd"]), 0, 1, _p(film_a), film_an, CHUNK, _p(ws.slab), s)
-        if mode == 2:  # FiLM2 sums -> d cemb2 / d temb2 (per sample)
-            lb.cdm_slab_sum_nc(_p(ws.slab), B, nch, 5, 2, C, _p(ws.d_emb["contextembed2"]), s)
-            lb.cdm_slab_sum_nc(_p(ws.slab), B, nch, 5, 3, C, _p(ws.d_emb["timeembed2"]), s)
         co = ws.coef
         bn = l.bn
-        nparts = fold(ws, _p(ws.slab), B * nch, 5, C, s)
+        if l.name in ws.sums_by:
+            # the sums came with the consumer's weight gradient (PreBnReluSums): one partial per split
+            assert mode == 0
+            nparts = fold(ws, _p(ws.sums), ws.sums_sp[l.name], 5, C, s)
+        else:
+            lb.cdm_norm_bwd_reduce(mode, g.p, g.ld, _p(y), C, B, S, S, C, _p(st["scale"]), _p(st["shift"]), 0,
+                                   _p(st["mean"]), _p(st["invstd"]), 0, 1, _p(film_a), film_an, CHUNK, _p(ws.slab), s)
+            if mode == 2:  # FiLM2 sums -> d cemb2 / d temb2 (per sample)
+                lb.cdm_slab_sum_nc(_p(ws.slab), B, nch, 5, 2, C, _p(ws.d_emb["contextembed2"]), s)
+                lb.cdm_slab_sum_nc(_p(ws.slab), B, nch, 5, 3, C, _p(ws.d_emb["timeembed2"]), s)
+            nparts = fold(ws, _p(ws.slab), B * nch, 5, C, s)
         lb.cdm_bn_bwd_finalize(_p(ws.dpart), nparts, C, float(B * S * S), _p(P[bn + ".weight"]), _p(st["invstd"]),
                                _p(G[bn + ".weight"]), _p(G[bn + ".bias"]), _p(co[0]), _p(co[1]), _p(co[2]),
                                _p(G[l.b]), s)
@@ -687,24 +704,27 @@ class UNetEngine:
         if l.name in ws.fused:
             # dy = bn_bwd(g, y) inside the staging of both convs; its scale from a bound on max|dy|
             dslot = self._slot(ws, "dy:" + l.name)
-            lb.cdm_bn_bwd_amax_bound(C, _p(co[0]), _p(co[1]), _p(co[2]), _p(st["mean"]), _p(st["invstd"]),
-                                     self._slot(ws, "g:" + l.name), self._slot(ws, "y:" + l.name), dslot, s)
+            if self.h3:
+                lb.cdm_bn_bwd_amax_bound(C, _p(co[0]), _p(co[1]), _p(co[2]), _p(st["mean"]), _p(st["invstd"]),
+                                         self._slot(ws, "g:" + l.name), self._slot(ws, "y:" + l.name), dslot, s)
             coef = (_p(st["scale"]), _p(st["shift"]), _p(st["mean"]), _p(st["invstd"]), _p(co[0]), _p(co[1]),
                     _p(co[2]))
             src, pre = self._src_pre(ws, l)
             sp = wgrad_splits(B * S * S, C, 9 * l.cin)
-            if pre is None:
-                lb.cdm_conv3x3_wgrad_h3_bnbwd(g.p, g.ld, _p(y), C, *coef, C, src.p, B, S, S, l.cin, src.ld, dslot,
-                                              self._src_slot(ws, l), sp, _p(ws.slab), s)
-            else:
-                lb.cdm_conv3x3_wgrad_h3_ex(g.p, g.ld, _p(y), C, *coef, C, src.p, B, S, S, l.cin, src.ld, pre[0],
-                                           pre[1], dslot, self._src_slot(ws, l), sp, _p(ws.slab), s)
-            lb.cdm_slab_reduce(_p(ws.slab), sp, C, 9 * l.cin, _p(G[l.w]), 9 * l.cin, 1, 9, l.cin, 0, 1.0, s)
+            # dgrad first: it writes the producer's g, which the weight gradient's producer sums read
             dgd = ws.dgrad_dst[l.name]
             key = l.name + ".wdg"
-            lb.cdm_conv3x3_dgrad_h3_bnbwd(g.p, g.ld, _p(y), C, *coef, B, S, S, C, _p(self.pk[key + "_x"]), dslot,
-                                          _p(self.pk[key + "_amax"]), dgd.p, dgd.ld, l.cin,
-                                          EPI_ACCUM if ws.dgrad_accum[l.name] else 0, gslot, s)
+            lb.cdm_conv3x3_dgrad_x16_bnbwd(g.p, g.ld, _p(y), C, *coef, B, S, S, C, _p(self.pk[key + "_x"]), dslot,
+                                           self._wamax(key), dgd.p, dgd.ld, l.cin,
+                                           EPI_ACCUM if ws.dgrad_accum[l.name] else 0, gslot, self.nterm, s)
+            if pre is None:
+                lb.cdm_conv3x3_wgrad_x16_bnbwd(g.p, g.ld, _p(y), C, *coef, C, src.p, B, S, S, l.cin, src.ld, dslot,
+                                               self._src_slot(ws, l), sp, _p(ws.slab), self.nterm, s)
+            else:
+                lb.cdm_conv3x3_wgrad_x16_ex(g.p, g.ld, _p(y), C, *coef, C, src.p, B, S, S, l.cin, src.ld, pre[0],
+                                            pre[1], *self._producer_sums(ws, l, sp), dslot, self._src_slot(ws, l), sp,
+                                            _p(ws.slab), self.nterm, s)
+            lb.cdm_slab_reduce(_p(ws.slab), sp, C, 9 * l.cin, _p(G[l.w]), 9 * l.cin, 1, 9, l.cin, 0, 1.0, s)
             return
         if l.cin == 1 and mode == 0 and self.fuse_cin1_bwd:
             # init_conv.conv1: only a weight gradient (the input needs none); its BN backward runs while that kernel
@@ -726,10 +746,12 @@ class UNetEngine:
             nparts = fold(ws, _p(ws.slab), B * _cdiv(S * S, CHUNK), 10, C, s)
             lb.cdm_slab_sum_all(_p(ws.dpart), nparts, 10, 0, 9, C, _p(G[l.w]), 1, 9, 0, s)
             return
-        self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s, amax_dy=dslot, amax_x=self._src_slot(ws, l), pre=pre)
         dgd = ws.dgrad_dst[l.name]
+        # dgrad first (it writes the producer's g, read by the producer sums of the weight gradient below)
         self.conv3x3(l.name + ".wdg", dy.p, B, S, C, dy.ld, None, dgd.p, dgd.ld, l.cin,
                      EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s, amax_x=dslot, amax_y=gslot)
+        self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s, amax_dy=dslot, amax_x=self._src_slot(ws, l), pre=pre,
+                       sums_of=l)
 
     def _src_pre(self, ws, l: "LayerSpec"):
         """(input activation, BN-ReLU transform or None) of conv l in train mode: a fused producer hands over its
@@ -752,23 +774,37 @@ class UNetEngine:
     # the dgrads that write the gradient wrt a ConvT output (gT1 / gT2) also record its max for the h3 ConvT bwd
     _CONVT_GRAD_PRODUCERS = {"up1.model.1.conv1": "up1.model.0", "up2.model.1.conv1": "up2.model.0"}
 
-    def _wgrad3x3(self, ws, dy: Act, x: Act, B, S, cin, cout, gW, s, amax_dy=None, amax_x=None, pre=None):
+    def _producer_sums(self, ws, l: "LayerSpec", sp: int):
+        """(x_g, ldxg, x_mean, x_invstd, x_sums) for conv l's weight gradient: the BN-backward sums of its fused producer
+        when they ride along (ws.sums_from), else all null."""
+        pn = ws.sums_from.get(l.name)
+        if pn is None:
+            return None, 0, None, None, None
+        g, st = ws.gout[pn], ws.bn[pn]
+        ws.sums_sp[pn] = sp * 3 * (l.cout // 128)     # one partial per block: split x kernel row x co tile
+        return g.p, g.ld, _p(st["mean"]), _p(st["invstd"]), _p(ws.sums)
+
+    def _wgrad3x3(self, ws, dy: Act, x: Act, B, S, cin, cout, gW, s, amax_dy=None, amax_x=None, pre=None,
+                  sums_of=None):
         lb = lib()
         sp = wgrad_splits(B * S * S, cout, 9 * cin)
-        if pre is not None:        # X = relu(x s + t) of a fused producer (h3, kernel-row weight gradient)
-            lb.cdm_conv3x3_wgrad_h3_ex(dy.p, dy.ld, None, 0, None, None, None, None, None, None, None, cout, x.p, B, S,
-                                       S, cin, x.ld, pre[0], pre[1], amax_dy, amax_x, sp, _p(ws.slab), s)
+        if pre is not None:        # X = relu(x s + t) of a fused producer (16-bit arithmetic, kernel-row weight gradient)
+            sums = self._producer_sums(ws, sums_of, sp) if sums_of is not None else (None, 0, None, None, None)
+            lb.cdm_conv3x3_wgrad_x16_ex(dy.p, dy.ld, None, 0, None, None, None, None, None, None, None, cout, x.p, B, S,
+                                        S, cin, x.ld, pre[0], pre[1], *sums, amax_dy, amax_x, sp, _p(ws.slab),
+                                        self.nterm, s)
             lb.cdm_slab_reduce(_p(ws.slab), sp, cout, 9 * cin, _p(gW), 9 * cin, 1, 9, cin, 0, 1.0, s)
             return
-        if self.nterm == NT_H3:
+        if self.x16:
             am = _p(self._amax)
-            if amax_dy is None:
+            if self.h3 and amax_dy is None:
                 amax_dy = am
                 lb.cdm_amax_f32(dy.p, B * S * S, cout, dy.ld, amax_dy, 0, s)
-            if amax_x is None:
+            if self.h3 and amax_x is None:
                 amax_x = am + 4
                 lb.cdm_amax_f32(x.p, B * S * S, cin, x.ld, amax_x, 0, s)
-            lb.cdm_conv3x3_wgrad_h3(dy.p, dy.ld, cout, x.p, B, S, S, cin, x.ld, amax_dy, amax_x, sp, _p(ws.slab), s)
+            lb.cdm_conv3x3_wgrad_x16(dy.p, dy.ld, cout, x.p, B, S, S, cin, x.ld, amax_dy, amax_x, sp, _p(ws.slab),
+                                     self.nterm, s)
         elif self.nterm:
             lb.cdm_conv3x3_wgrad_x3(dy.p, dy.ld, cout, x.p, B, S, S, cin, x.ld, sp, _p(ws.slab), self.nterm, s)
         else:
@@ -784,19 +820,20 @@ class UNetEngine:
         nparts = fold(ws, _p(ws.slab), B * _cdiv(Ho * Ho, CHUNK), 1, cout, s)
         lb.cdm_slab_sum_all(_p(ws.dpart), nparts, 1, 0, 1, cout, _p(G[name + ".bias"]), 0, 1, 0, s)
         sp = wgrad_splits(B * Hin * Hin, cin, 4 * cout)
-        h3 = self.nterm == NT_H3
-        if h3:
+        x16 = self.x16
+        if x16:
             prod = next(k for k, v in self._CONVT_GRAD_PRODUCERS.items() if v == name)
             a_gy = self._slot(ws, "gT:" + prod)
             a_x = self._slot(ws, {"up1.model.0": "catU1", "up2.model.0": "catU2"}[name])
-            lb.cdm_convT2x2_wgrad_h3(x.p, B, Hin, Hin, cin, x.ld, gy.p, cout, gy.ld, a_x, a_gy, sp, _p(ws.slab), s)
+            lb.cdm_convT2x2_wgrad_x16(x.p, B, Hin, Hin, cin, x.ld, gy.p, cout, gy.ld, a_x, a_gy, sp, _p(ws.slab),
+                                      self.nterm, s)
         else:
             lb.cdm_convT2x2_wgrad(x.p, B, Hin, Hin, cin, x.ld, gy.p, cout, gy.ld, sp, _p(ws.slab), s)
         # slab[z][ci][ij*cout+co] -> [ci][co][ij]
         lb.cdm_slab_reduce(_p(ws.slab), sp, cin, 4 * cout, _p(G[name + ".weight"]), 4 * cout, 1, 4, cout, 0, 1.0, s)
-        if h3:
-            lb.cdm_convT2x2_dgrad_h3(gy.p, B, Hin, Hin, cout, gy.ld, _p(self.pk[name + ".wtT_x"]), a_gy,
-                                     _p(self.pk[name + ".wtT_amax"]), dx.p, dx.ld, cin, 0, s)
+        if x16:
+            lb.cdm_convT2x2_dgrad_x16(gy.p, B, Hin, Hin, cout, gy.ld, _p(self.pk[name + ".wtT_x"]), a_gy,
+                                      self._wamax(name + ".wtT"), dx.p, dx.ld, cin, 0, self.nterm, s)
         else:
             lb.cdm_convT2x2_dgrad(gy.p, B, Hin, Hin, cout, gy.ld, _p(self.pk[name + ".wtT"]), dx.p, dx.ld, cin, 0, s)
 
@@ -990,8 +1027,21 @@ class Workspace:
                 elif l.cin > 1:
                     self.dgrad_dst[l.name], self.dgrad_accum[l.name] = Act(Gb, l.cin), False
             self._wire_fused_bn_bwd(eng, L, kinds)
+            # producer BN-backward sums in the consumer's weight gradient: a fused (BN-ReLU staged) dense producer p
+            # whose consumer c takes the kernel-row weight gradient with the X transform
+            self.sums_from, self.sums_by, self.sums_sp = {}, {}, {}
+            if eng.fuse_bn_sums:
+                for i in range(1, len(L)):
+                    p_, c_ = L[i - 1], L[i]
+                    if p_.name in self.fused_fwd and kinds[p_.name] == "dense" and c_.cin % 128 == 0 \
+                            and c_.cout % 128 == 0 and c_.S % 16 == 0:
+                        self.sums_from[c_.name], self.sums_by[p_.name] = p_.name, c_.name
+            nsum = max([wgrad_splits(B * L[i].S * L[i].S, L[i].cout, 9 * L[i].cin) * 3 * (L[i].cout // 128) * 5
+                        * L[i].cin for i in range(len(L)) if L[i].name in self.sums_from] + [1])
+            self.sums = E(nsum)
         else:
             self.fused, self.g_amax_key, self.out0_g_key = set(), {}, None
+            self.sums_from, self.sums_by, self.sums_sp = {}, {}, {}
 
     def ymm_of(self, l) -> tuple:
         """(pointer, ld) of fused layer l's max keys; its min keys sit ld ints further."""

@@ -97,6 +97,49 @@ int cdm_conv3x3_wgrad_h3_ex(const float* g, int ldg, const float* y, int ldy, co
                             int Cout, const float* x, int N, int H, int W, int Cin, int ldx, const float* x_s,
                             const float* x_t, const float* amax_dy, const float* amax_x, int splits, float* slab,
                             void* stream);
+/* ---- the 16-bit-arithmetic ("x16") forms of the h3 entry points above and of the h3 ConvT 2x2 calls below ----------
+ * identical contracts plus a trailing `nterm`: NT_H3 = 4 (fp32-class scaled fp16 hi/lo, = the *_h3 call) or 1 (one
+ * bf16 term per operand, fp32 accumulate: BASELINE configuration C4, bf16 mixed precision, with every train-mode
+ * Conv -> BatchNorm -> ReLU fusion of the h3 path).  For nterm = 1 the weight images come from cdm_split_bf16x3 (plane
+ * 0 is read) and the amax_* operand maxima are ignored (may be null).  Reference ops: nn.Conv2d(.,.,3,1,1)
+ * diffusion_utilities.py:27,34 and its autograd; nn.ConvTranspose2d(Cin, Cout, 2, 2) diffusion_utilities.py:86. */
+int cdm_conv3x3_fwd_x16(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
+                        const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags, float* stats,
+                        int stats_ld, int kc, float* amax_y, int nterm, void* stream);
+int cdm_conv3x3_fwd_x16_ex(const float* x, int N, int H, int W, int Cin, int ldx, const float* pre_s, const float* pre_t,
+                           const void* wx, const float* amax_x, const float* amax_w, const float* bias, float* y,
+                           int ldy, int Cout, int flags, float* stats, int stats_ld, int kc, float* amax_y, int* ymm,
+                           int ymm_ld, int nterm, void* stream);
+int cdm_conv3x3_wgrad_x16(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,
+                          const float* amax_dy, const float* amax_x, int splits, float* slab, int nterm, void* stream);
+int cdm_conv3x3_dgrad_x16_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
+                                const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
+                                int N, int H, int W, int C, const void* wx, const float* amax_dy, const float* amax_w,
+                                float* out, int ldo, int Cout, int flags, float* amax_out, int nterm, void* stream);
+int cdm_conv3x3_wgrad_x16_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
+                                const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
+                                int Cout, const float* x, int N, int H, int W, int Cin, int ldx, const float* amax_dy,
+                                const float* amax_x, int splits, float* slab, int nterm, void* stream);
+/* cdm_conv3x3_wgrad_x16_ex also takes (x_g, ldxg, x_mean, x_invstd, x_sums), all optional (x_sums null: off): with
+ * x_s / x_t given, the BatchNorm-backward channel sums of the layer that produced x are accumulated while x is staged:
+ * g_pre = (x x_s + x_t > 0 ? x_g : 0), xhat = (x - x_mean) x_invstd; x_sums[(split * 3 + kernel row) * (Cout / 128) +
+ * co tile][5][Cin] (one partial per block, splits = effective split count) rows 0 = sum g_pre, 1 = sum g_pre xhat,
+ * 4 = sum xhat (rows 2, 3 zero) — the slab of cdm_norm_bwd_reduce mode 0 with 3 Cout/128 tiles per split
+ * (x_g = the gradient wrt this conv's input, written by this layer's dgrad before this call). */
+int cdm_conv3x3_wgrad_x16_ex(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
+                             const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
+                             int Cout, const float* x, int N, int H, int W, int Cin, int ldx, const float* x_s,
+                             const float* x_t, const float* x_g, int ldxg, const float* x_mean, const float* x_invstd,
+                             float* x_sums, const float* amax_dy, const float* amax_x, int splits, float* slab,
+                             int nterm, void* stream);
+int cdm_convT2x2_fwd_x16(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
+                         const float* amax_w, const float* bias, float* y, int ldy, int Cout, float* amax_y, int nterm,
+                         void* stream);
+int cdm_convT2x2_dgrad_x16(const float* dy, int N, int H, int W, int Cout, int lddy, const void* wx,
+                           const float* amax_dy, const float* amax_w, float* dx, int lddx, int Cin, int flags, int nterm,
+                           void* stream);
+int cdm_convT2x2_wgrad_x16(const float* x, int N, int H, int W, int Cin, int ldx, const float* dy, int Cout, int lddy,
+                           const float* amax_x, const float* amax_dy, int splits, float* slab, int nterm, void* stream);
 /* fp32 [K][N] (ld ldb) -> [ceil(K/16)][3][N][16]: planes 0/1 = fp16 hi/lo of b * 2^(14-e), max|b| = *amax < 2^e */
 int cdm_split_f16x2(const float* b, long long ldb, int K, int N, const float* amax, void* out, void* stream);
 /* batched train-mode repack: jobs_dev = device array of njobs records

@@ -27,6 +27,7 @@ import torch
 import torch.nn.functional as F
 
 from oracle import ref_cpu as R
+import _parity
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -68,20 +69,29 @@ def _forward_pair(nf, H, B, math, seed=3):
 
 
 class _bf16_operands:
-    """Oracle hook: round every 3x3 conv's input and weights to bf16 (fp32 accumulate), as C4 does."""
+    """Oracle hook: round the operands of every 3x3 conv with C_in > 1 and of the two ConvTranspose2d(k=2, s=2) to bf16
+    (fp32 accumulate), as C4 does (the C_in = 1 / C_out = 1 convs and up0 stay fp32 on both sides)."""
 
     def __enter__(self):
-        self.orig = R.F.conv2d
+        self.orig, self.orig_t = R.F.conv2d, R.F.conv_transpose2d
+
+        def bf(v):
+            return v.to(torch.bfloat16).to(v.dtype)
 
         def conv(x, w, b=None, *a, **k):
             if w.shape[-1] == 3 and w.shape[1] > 1:
-                x, w = x.to(torch.bfloat16).to(x.dtype), w.to(torch.bfloat16).to(w.dtype)
+                x, w = bf(x), bf(w)
             return self.orig(x, w, b, *a, **k)
-        R.F.conv2d = conv
+
+        def convt(x, w, b=None, *a, **k):
+            if w.shape[-1] == 2:
+                x, w = bf(x), bf(w)
+            return self.orig_t(x, w, b, *a, **k)
+        R.F.conv2d, R.F.conv_transpose2d = conv, convt
         return self
 
     def __exit__(self, *exc):
-        R.F.conv2d = self.orig
+        R.F.conv2d, R.F.conv_transpose2d = self.orig, self.orig_t
 
 
 def _grad_errors(nf, H, B, math, seed=4, emulate_bf16=False):
@@ -172,6 +182,98 @@ def test_c4_bf16_cfg_sampler_vs_reference_golden(w):
     print(f"w={w:g}: final hip {e_hip:.2e} oracle-bf16 {e_emu:.2e}; snapshots hip {ei_hip:.2e} oracle-bf16 {ei_emu:.2e}")
     assert e_hip <= max(1.5 * e_emu, 1e-3), (e_hip, e_emu)
     assert ei_hip <= max(1.5 * ei_emu, 1e-3), (ei_hip, ei_emu)
+
+
+def test_c4_bf16_trainer_step_vs_emulated_oracle():
+    """The C4 Trainer step bench.py times (bf16 arithmetic, fused BN / ConvT paths, Adam), one injected step at nf=64,
+    B=4: gradients and post-Adam parameters vs the fp64 oracle within 1.5x the error of the reference run under the
+    same bf16 operand rounding (_bf16_operands), the bar of test_c4_bf16_train_grads_vs_fp64 (statistics over every
+    parameter); the loss, one scalar whose bf16 error is a random-sign sum over the batch, within 3x the emulated
+    reference's (measured 2.2x)."""
+    from cdm_amd import Trainer
+    nf, B, T, lr = 64, 4, 1500, 1e-4
+    m = _model(nf, seed=7, math="bf16").train()
+    sd = R.clone_sd(m.state_dict())
+    g = torch.Generator().manual_seed(31)
+    x = torch.rand(B, 1, 64, 64, generator=g); c = torch.rand(B, 6, generator=g)
+    noise = torch.randn(B, 1, 64, 64, generator=g); tt = torch.randint(1, T + 1, (B,), generator=g)
+    sc = torch.rand(2 * nf, generator=g) * 2 - 1
+    tr = Trainer(m, lr, T, B, use_graph=False)
+    loss = float(tr.step(x.cuda(), c.cuda(), inject=(noise.cuda(), tt.cuda().int(), sc.cuda())).item())
+    torch.cuda.synchronize()
+    grads = {n: v.detach().cpu().double() for n, v in tr.grads.items()}
+    post = {n: v.detach().cpu().double() for n, v in tr.views.items()}
+    _, _, ab = R.make_schedule(T)
+
+    def oracle(dtype, emulate):
+        s = {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+        otr = R.OracleTrainer(s, n_feat=nf, n_cfeat=6, height=64, lr=lr)
+        w, b = sc[:nf].reshape(nf, 1, 1, 1).to(dtype), sc[nf:].to(dtype)
+        args = (x.to(dtype), c.to(dtype), noise.to(dtype), tt, T, ab.to(dtype), (w, b))
+        if emulate:
+            with _bf16_operands():
+                l, _, gr = otr.step(*args)
+        else:
+            l, _, gr = otr.step(*args)
+        return float(l), gr, {k: v.detach().clone() for k, v in otr.sd.items()}
+    l64, g64, sd64 = oracle(torch.float64, False)
+    le, ge, sde = oracle(torch.float32, True)
+    keep = [n for n in grads if not (".conv1.0.bias" in n or ".conv2.0.bias" in n)]
+    eh = {n: ((grads[n] - g64[n]).norm() / g64[n].norm()).item() for n in keep}
+    ee = {n: ((ge[n].double() - g64[n]).norm() / g64[n].norm()).item() for n in keep}
+    dh = np.concatenate([((post[n] - sd64[n]) / lr).abs().numpy().ravel() for n in keep])
+    de = np.concatenate([((sde[n].double() - sd64[n]) / lr).abs().numpy().ravel() for n in keep])
+    rh, re_ = float(np.sqrt((dh ** 2).mean())), float(np.sqrt((de ** 2).mean()))
+    res = dict(loss_err=abs(loss - l64), loss_err_emulated=abs(le - l64), grad_max=max(eh.values()),
+               grad_max_emulated=max(ee.values()), grad_median=float(np.median(list(eh.values()))),
+               grad_median_emulated=float(np.median(list(ee.values()))), param_dev_lr_rms=rh,
+               param_dev_lr_rms_emulated=re_)
+    _parity.record("c4_bf16_trainer_step", n_feat=nf, B=B, **res)
+    print(res)
+    assert res["loss_err"] <= 3 * res["loss_err_emulated"] + 1e-6
+    assert res["grad_max"] <= 1.5 * res["grad_max_emulated"]
+    assert res["grad_median"] <= 1.5 * res["grad_median_emulated"]
+    assert rh <= 1.5 * re_ + 1e-3
+
+
+@pytest.mark.parametrize("w", [0.0, 3.0])
+def test_c4_bf16_cfg_T1500_vs_emulated_oracle(w):
+    """bf16 sampling at the benchmarked T=1500 (w=0 and the CFG w=3), CPU-RNG replay of the reference's run
+    (tests/golden/sampler_T1500_nf8.npz): the deviation from the reference's fp64 trajectory, RMS over the final x and
+    the 13 stored snapshots (each relative to its max|x|), within 1.5x that of the reference's own sampler run under
+    the same bf16 operand rounding (the CPU oracle with _bf16_operands, same RNG replay), at least 1e-3."""
+    import cdm_amd
+    sfx = np.load(os.path.join(GOLD, "sampler_T1500_nf8.npz"))
+    T = int(sfx["T"])
+    fx = np.load(os.path.join(GOLD, "model_nf8.npz"))
+    sd = {k[3:]: torch.from_numpy(fx[k].copy()) for k in fx.files if k.startswith("sd.")}
+    m = cdm_amd.ContextUnet(1, 8, 6, 64, conv_math="bf16")
+    m.load_state_dict(sd)
+    m = m.cuda().eval()
+    d = cdm_amd.DDPM(m, T, "cuda", z_source="host")
+    seed = int(sfx[f"w{w:g}_seed"])
+    torch.manual_seed(seed)
+    x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(sfx["params"]), w)
+    with _bf16_operands():
+        torch.manual_seed(seed)
+        xe, inte = R.sample_ddpm(R.make_model_fn(R.clone_sd(sd), n_feat=8, n_cfeat=6, height=64), 2, 64,
+                                 torch.from_numpy(sfx["params"]), w, T, R.make_schedule(T), 6)
+    keep = sfx["snap_keep"]
+
+    def errs(final, snaps):
+        out = [float(np.abs(np.asarray(final) - sfx[f"w{w:g}_x_fp64"]).max() / np.abs(sfx[f"w{w:g}_x_fp64"]).max())]
+        for j, s in enumerate(keep):
+            r = sfx[f"w{w:g}_inter_fp64"][j]
+            out.append(float(np.abs(np.asarray(snaps[s]) - r).max() / np.abs(r).max()))
+        return np.array(out)
+    eh = errs(x.cpu().numpy(), inter)
+    ee = errs(xe.numpy(), inte.numpy())
+    rh, re_ = float(np.sqrt((eh ** 2).mean())), float(np.sqrt((ee ** 2).mean()))
+    _parity.record("c4_bf16_sample_T1500", w=w, rms_err=rh, rms_err_emulated=re_, final_err=float(eh[0]),
+                   final_err_emulated=float(ee[0]))
+    print(f"T=1500 bf16 w={w:g}: RMS deviation from fp64 HIP {rh:.3e}, emulated reference {re_:.3e}; final "
+          f"{eh[0]:.3e} / {ee[0]:.3e}")
+    assert rh <= max(1.5 * re_, 1e-3)
 
 
 # ------------------------------------------------------------------------------------------ C5 (256x256)

@@ -593,3 +593,54 @@ def test_up0_large_map_input_gradient(L, B, C, k):
     L.cdm_slab_reduce(slab.data_ptr(), sp, B, C, dx.data_ptr(), C, 0, 1, C, 0, 1.0, _s())
     torch.cuda.synchronize()
     _close(dx, x.grad.reshape(B, C))
+
+
+@pytest.mark.parametrize("nterm", [4, 1])
+@pytest.mark.parametrize("B,S,cin,cout", [(2, 64, 128, 128), (4, 64, 128, 128), (2, 32, 256, 256), (2, 32, 128, 256),
+                                          (3, 32, 128, 128), (16, 64, 128, 128)])
+def test_producer_bn_sums_in_wgrad(B, S, cin, cout, nterm):
+    """cdm_conv3x3_wgrad_x16_ex with x_sums (PreBnReluSums): the producer's BatchNorm-backward sums accumulated while
+    the weight gradient stages X = relu(y s + t) — S1 = sum g_pre, S2 = sum g_pre xhat, S5 = sum xhat per channel —
+    vs the same sums in fp64 on the host, <= 1e-5 relative (fp32 partials per split, folded in fp64), for both 16-bit
+    arithmetics and every K-step size (16, 32, 64 pixels per barrier: the shapes pick them); every block's partial row
+    written (each X pixel is summed by exactly one of the 3 x gx blocks that stage it).
+    The weight gradient itself must equal the call without sums bit for bit."""
+    import cdm_amd
+    from cdm_amd.engine import wgrad_splits
+    L = cdm_amd.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device="cuda").manual_seed(5)
+    P = B * S * S
+    y = torch.randn(P, cin, device="cuda", generator=g)
+    gx = torch.randn(P, cin, device="cuda", generator=g)
+    dy = torch.randn(P, cout, device="cuda", generator=g) * 1e-2
+    s_ = torch.rand(cin, device="cuda", generator=g) + 0.5
+    t_ = torch.randn(cin, device="cuda", generator=g) * 0.1
+    mean = torch.randn(cin, device="cuda", generator=g) * 0.1
+    inv = torch.rand(cin, device="cuda", generator=g) + 0.5
+    am = torch.ones(4, device="cuda") * 8.0
+    sp = wgrad_splits(P, cout, 9 * cin)
+    nt = sp * 3 * (cout // 128)                     # one partial per block: split x kernel row x co tile
+    slabs = []
+    sums = torch.full((nt * 5 * cin,), float("nan"), device="cuda")
+    for with_sums in (True, False):
+        slab = torch.empty(sp * cout * 9 * cin, device="cuda")
+        L.cdm_conv3x3_wgrad_x16_ex(dy.data_ptr(), cout, None, 0, None, None, None, None, None, None, None, cout,
+                                   y.data_ptr(), B, S, S, cin, cin, s_.data_ptr(), t_.data_ptr(),
+                                   gx.data_ptr() if with_sums else None, cin, mean.data_ptr() if with_sums else None,
+                                   inv.data_ptr() if with_sums else None, sums.data_ptr() if with_sums else None,
+                                   am.data_ptr(), am.data_ptr() + 4, sp, slab.data_ptr(), nterm, st)
+        slabs.append(slab)
+    torch.cuda.synchronize()
+    assert torch.equal(slabs[0], slabs[1])
+    sm = sums.view(nt, 5, cin)
+    assert not torch.isnan(sm).any()
+    got = sm.double().sum(0)
+    zp = y * s_ + t_
+    gp = torch.where(zp > 0, gx, torch.zeros_like(gx)).double()
+    xh = ((y - mean) * inv).double()
+    ref = torch.stack([gp.sum(0), (gp * xh).sum(0), xh.sum(0)])
+    g3 = torch.stack([got[0], got[1], got[4]])
+    err = ((g3 - ref).abs().max(dim=1).values / ref.abs().max(dim=1).values).max().item()
+    assert err <= 1e-5, err
+    assert float(got[2].abs().max()) == 0 and float(got[3].abs().max()) == 0

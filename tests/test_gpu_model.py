@@ -270,6 +270,7 @@ def test_fused_bn_fwd_bit_exact_nf128(B):
     import cdm_amd.model as M
     eng = M.get_engine(nf, 6, 64, torch.device("cuda", torch.cuda.current_device()), "h3")
     res = []
+    eng.fuse_bn_sums = False      # (the producer sums ride on the fused X staging: same sums, other summation order)
     try:
         for fuse in (True, False):
             eng.fuse_bn_fwd = fuse
@@ -284,9 +285,59 @@ def test_fused_bn_fwd_bit_exact_nf128(B):
                         {k: v.detach().cpu() for k, v in m.state_dict().items() if "running" in k}))
     finally:
         eng.fuse_bn_fwd = True
+        eng.fuse_bn_sums = True
         M._WS.clear()
     assert torch.equal(res[0][0], res[1][0])
     for k in res[1][1]:
         assert torch.equal(res[0][1][k], res[1][1][k]), k
     for k in res[1][2]:
         assert torch.equal(res[0][2][k], res[1][2][k]), k
+
+
+@pytest.mark.parametrize("math", ["h3", "bf16"])
+def test_bn_sums_in_consumer_wgrad_nf128(math):
+    """The BatchNorm-backward channel sums of each fused dense producer computed in its consumer's weight-gradient X
+    staging (PreBnReluSums, one partial per split) vs the separate cdm_norm_bwd_reduce pass ($CDM_FUSE_BN_SUMS=0), n_feat
+    128, B=3: the forward (eps, running statistics) is untouched (bit-identical); the gradients differ only by the sums'
+    fp32 summation order, which moves the BN-backward coefficients by rounding: relative L2 per gradient <= 1e-2 (the
+    kink flips of test_train_grads_random_weights_vs_fp64), median <= 1e-4 under h3; under bf16 a last-bit change of
+    a coefficient flips the bf16 rounding of dy elements, so max <= 5e-2, median <= 5e-3 (the bf16 operand noise of
+    the reference itself is ~0.3 relative L2 median on such gradients, test_c4_bf16_train_grads_vs_fp64; measured
+    1.25e-2 / 2.0e-3)."""
+    nf, B, T = 128, 3, 1500
+    g = torch.Generator().manual_seed(17)
+    x = torch.rand(B, 1, 64, 64, generator=g); noise = torch.randn(B, 1, 64, 64, generator=g)
+    c = torch.rand(B, 6, generator=g); tt = torch.randint(1, T + 1, (B,), generator=g)
+    _, _, ab = R.make_schedule(T)
+    xp = R.perturb_input(x, tt, noise, ab)
+    import cdm_amd.model as M
+    eng = M.get_engine(nf, 6, 64, torch.device("cuda", torch.cuda.current_device()), math)
+    res = []
+    try:
+        for on in (True, False):
+            eng.fuse_bn_sums = on
+            M._WS.clear()
+            m = _model(nf, seed=18, math=math).train()
+            torch.manual_seed(36)
+            pred = m(xp.cuda(), (tt / T).cuda(), c.cuda())
+            F.mse_loss(pred, noise.cuda()).backward()
+            ws = eng.workspace(B, True)
+            assert len(ws.sums_from) == (13 if on else 0), sorted(ws.sums_from)
+            res.append((pred.detach().cpu(), {k: p.grad.detach().double().cpu() for k, p in m.named_parameters()},
+                        {k: v.detach().cpu() for k, v in m.state_dict().items() if "running" in k}))
+    finally:
+        eng.fuse_bn_sums = True
+        M._WS.clear()
+    assert torch.equal(res[0][0], res[1][0])
+    for k in res[1][2]:
+        assert torch.equal(res[0][2][k], res[1][2][k]), k
+    errs = []
+    for k, ref in res[1][1].items():
+        if ".conv1.0.bias" in k or ".conv2.0.bias" in k or ref.norm() == 0:
+            continue
+        errs.append(((res[0][1][k] - ref).norm() / ref.norm()).item())
+    print(f"[{math}] sums in wgrad vs separate pass: rel L2 max {max(errs):.2e} median {float(np.median(errs)):.2e}")
+    if math == "h3":
+        assert max(errs) <= 1e-2 and float(np.median(errs)) <= 1e-4
+    else:
+        assert max(errs) <= 5e-2 and float(np.median(errs)) <= 5e-3

@@ -368,7 +368,7 @@ def test_nonfinite_loss_guard():
 
 # seed of the inputs of test_trainer_three_steps_all_arithmetics: chosen (tools/trainer_seed_scan.py on the GPU box) so
 # that no arithmetic flips a ReLU / MaxPool kink in these three steps — the trajectory bar then holds for each one
-KINK_FREE_SEED = 3
+KINK_FREE_SEED = 5
 
 
 def trainer_three_steps(math, seed, nf=8, B=4, T=1000, lrs=(1e-3, 1e-3, 7.5e-4)):
@@ -411,7 +411,8 @@ def trainer_three_steps(math, seed, nf=8, B=4, T=1000, lrs=(1e-3, 1e-3, 7.5e-4))
             ge32.append(((g32[n].double() - g64[n]).norm() / g64[n].norm()).item())
         post = _params(tr)
         h = _dev_stats(post, sd64, keep, lrs[0]); r = _dev_stats(sd32, sd64, keep, lrs[0])
-        bn_h = max((v.double() - sd64[kk]).abs().max().item() for kk, v in m.state_dict().items() if "running" in kk)
+        bn_h = max((v.detach().cpu().double() - sd64[kk]).abs().max().item() for kk, v in m.state_dict().items()
+                   if "running" in kk)
         bn_r = max((sd32[kk].double() - sd64[kk]).abs().max().item() for kk in sd64 if "running" in kk)
         out.append(dict(step=k, loss_err=abs(loss - l64), loss_err_ref32=abs(l32 - l64), loss64=l64,
                         grad_max=max(ge), grad_max_ref32=max(ge32), grad_median=float(np.median(ge)),

@@ -14,9 +14,10 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=60)
 ap.add_argument("--w", type=float, default=0.0)
 ap.add_argument("--n", type=int, default=256)
+ap.add_argument("--math", default="h3")
 a = ap.parse_args()
 import cdm_amd  # noqa: E402
 torch.manual_seed(0)
-model = cdm_amd.ContextUnet(1, bench.NF, bench.NCF, bench.H).cuda().eval()
+model = cdm_amd.ContextUnet(1, bench.NF, bench.NCF, bench.H, conv_math=a.math).cuda().eval()
 ms, S = bench.sample_rate(model, bench.T, a.n, a.w, a.steps, 0, torch.cuda.synchronize)
 print(f"sample {ms:.3f} ms per denoise step (n={a.n}, w={a.w:g}, {S} steps)")
