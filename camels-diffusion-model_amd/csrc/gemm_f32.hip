@@ -855,7 +855,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
                                                                       int ldx, const __bf16* __restrict__ wx3,
                                                                       int Cout, const float* amax_x,
                                                                       const float* amax_w, EP ep, PRE pre,
-                                                                      int mtiles, int tpb) {
+                                                                      int mtiles, int tpb, int stg = 0) {
     constexpr int NS = XTerms<NT>::NS;
     constexpr int ROWS = HBM_ / WT, HR = ROWS + 2, HC = WT + 2, HPX = HR * HC;
     constexpr int HQ = (HPX * 4 + HTHREADS - 1) / HTHREADS;   // float4 halo pieces per thread
@@ -1204,7 +1204,10 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         // dy = 2: fetch B of the next chunk's dy = 0; split + store the next halo (buffer idle since chunk cc-1)
         // ahead of this group's MFMAs, so its VALU work interleaves with them; B after them (just issued)
         gload_b(morec ? g0 + 3 : 0, bregA);
-        const bool late = (ABL & 256) && wave < 4;   // staggered split: wave-uniform
+        // staggered split (ABL 256, or stg at run time: $CDM_HALO_STAGGER): waves 0-3 split + store the next halo
+        // after this kernel row's MFMAs, waves 4-7 before them, so each SIMD pairs one wave's VALU with its partner's
+        // MFMAs (wave-uniform)
+        const bool late = ((ABL & 256) || stg) && wave < 4;
         if constexpr (!(ABL & 1024)) {
             if (morec && !late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
         }
@@ -1409,7 +1412,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
                                                               const float* __restrict__ x, int H, int W, int Cin,
                                                               int ldx, int ktiles, int kt_per_split,
                                                               const float* amax_dy, const float* amax_x,
-                                                              float* __restrict__ slab, PRE pre, PX px) {
+                                                              float* __restrict__ slab, PRE pre, PX px, int stg) {
     constexpr int NS = XTerms<NT>::NS;
     constexpr int RA = 16 * KS, RB = RA + 2;          // image rows (pixels): dY, X with its halo
     constexpr int IA = RA * 128, IB = RB * 128;       // bf16 per term image
@@ -1584,6 +1587,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
         if (more) gload();
         const char* a = reinterpret_cast<const char*>(smem + cur * STEP);
         const char* b = a + NS * IA * 2;
+        auto mma = [&]() {
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
         bf16x8 fa[2][NS];
@@ -1620,7 +1624,17 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
             }
         }
         }
-        if (more) sstore(smem + (cur ^ 1) * STEP);
+        };
+        // stg: the two waves of each SIMD (w, w + 4) run the step in opposite orders — one stages the next K step
+        // (VALU: BN transforms, term split, LDS writes) while the other issues its MFMAs, instead of both
+        // alternating in lock-step between the barriers
+        if (stg && wave >= 4) {
+            if (more) sstore(smem + (cur ^ 1) * STEP);
+            mma();
+        } else {
+            mma();
+            if (more) sstore(smem + (cur ^ 1) * STEP);
+        }
         __syncthreads();
         cur ^= 1;
     }
@@ -1673,6 +1687,14 @@ static int halo_tpb(int mtiles, int ntiles, int nterm, int wt) {
     return t < 1 ? 1 : (t > 8 ? 8 : t);
 }
 
+// the staggered halo split of the LDS-halo conv: on for h3, off for the one-term bf16 images ($CDM_HALO_STAGGER=0 / 1
+// forces it).  Same-box A/B, 2 rounds (profiles/r3_ab_halo_stagger.txt): C2 (h3) train step 51.92-51.95 -> 51.34-51.44
+// ms; C4 (bf16) 32.20-32.21 -> 32.26-32.40 ms (its halo split is a plain conversion: nothing left to hide)
+static int halo_stagger(int nterm) {
+    static const int v = [] { const char* e = getenv("CDM_HALO_STAGGER"); return e ? atoi(e) : -1; }();
+    return v >= 0 ? v : (nterm == NT_H3 ? 1 : 0);
+}
+
 template <int WT, class PRE = PreNone>
 static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
                             const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm, hipStream_t s,
@@ -1690,18 +1712,18 @@ static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, cons
         // LDS fits the two-term (h3) image only (WT 256: 2 x 2 x 774 px x 32 B + 48 KiB B = 145 KiB)
         if (nterm != NT_H3) return (int)hipErrorInvalidValue;
         hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EpiStoreW<4>, true, 1, PRE>), grid, dim3(HTHREADS), 0, s,
-                           x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb);
+                           x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm));
         return cdm_status();
     } else {
     switch (nterm) {
         case 1: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, (1 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb); break;
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
         case 3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<3, WT, EpiStoreW<4>, true, (3 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb); break;
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
         case NT_H3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EpiStoreW<4>, true, (NT_H3 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0,
-                                       s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb); break;
+                                       s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
         case 6: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<6, WT, EpiStoreW<4>, true, (6 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb); break;
+                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();
@@ -2121,6 +2143,14 @@ CDM_API int cdm_conv3x3_fwd_h3_ex(const float* x, int N, int H, int W, int Cin, 
                                   stats, stats_ld, kc, amax_y, ymm, ymm_ld, NT_H3, stream);
 }
 
+// the staggered wave order of the kernel-row weight gradient ($CDM_WGRAD_STAGGER=1; off: same-box A/B, 2 rounds,
+// C2 train step 52.11-52.42 -> 52.88-53.05 ms and C4 32.26-32.52 -> 33.38-33.61 ms with it on — the staging wave
+// then waits on the K step's loads it has just issued, profiles/r3_ab_wgrad_stagger.txt)
+static int wgrad_stagger() {
+    static const int v = [] { const char* e = getenv("CDM_WGRAD_STAGGER"); return e ? atoi(e) : 0; }();
+    return v;
+}
+
 template <int KS, class PRE = PreNone, class PX = PreNone>
 static int launch_wgrad_row(const float* dy, int lddy, int Cout, const float* x, int H, int W, int Cin, int ldx, int K,
                             int sp, const float* amax_dy, const float* amax_x, float* slab, int nterm, hipStream_t st,
@@ -2130,29 +2160,29 @@ static int launch_wgrad_row(const float* dy, int lddy, int Cout, const float* x,
     if constexpr (KS == 4) {   // 64-pixel K steps: the one-term bf16 images only (66 KiB of LDS; h3 would need 133)
         if (nterm != 1) return (int)hipErrorInvalidValue;
         hipLaunchKernelGGL((wgrad3x3_row_kernel<1, 4, PRE, PX>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin,
-                           ldx, ktiles, per, amax_dy, amax_x, slab, pre, px);
+                           ldx, ktiles, per, amax_dy, amax_x, slab, pre, px, wgrad_stagger());
         return cdm_status();
     } else {
     if constexpr (PX::kind != 0) {            // the fused X transform: the 16-bit arithmetics (h3, bf16)
         if (nterm == NT_H3)
             hipLaunchKernelGGL((wgrad3x3_row_kernel<NT_H3, KS, PRE, PX>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H,
-                               W, Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px);
+                               W, Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px, wgrad_stagger());
         else if (nterm == 1)
             hipLaunchKernelGGL((wgrad3x3_row_kernel<1, KS, PRE, PX>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W,
-                               Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px);
+                               Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px, wgrad_stagger());
         else
             return (int)hipErrorInvalidValue;
         return cdm_status();
     }
     switch (nterm) {
         case 1: hipLaunchKernelGGL((wgrad3x3_row_kernel<1, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
-                                   ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}); break;
+                                   ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}, wgrad_stagger()); break;
         case 3: hipLaunchKernelGGL((wgrad3x3_row_kernel<3, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
-                                   ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}); break;
+                                   ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}, wgrad_stagger()); break;
         case NT_H3: hipLaunchKernelGGL((wgrad3x3_row_kernel<NT_H3, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W,
-                                       Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}); break;
+                                       Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}, wgrad_stagger()); break;
         case 6: hipLaunchKernelGGL((wgrad3x3_row_kernel<6, KS, PRE>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin, ldx,
-                                   ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}); break;
+                                   ktiles, per, amax_dy, amax_x, slab, pre, PreNone{}, wgrad_stagger()); break;
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();

@@ -125,8 +125,11 @@ class UNetEngine:
         self.fuse_bn_fwd = self.x16 and os.environ.get("CDM_FUSE_BN_FWD", "1") != "0"
         # a fused producer's BN-backward channel sums accumulated in its consumer's weight-gradient X staging (which
         # stages the producer's y anyway), after the consumer's dgrad wrote the producer's g: no separate pass over g and
-        # y ($CDM_FUSE_BN_SUMS=0: cdm_norm_bwd_reduce)
-        self.fuse_bn_sums = self.x16 and os.environ.get("CDM_FUSE_BN_SUMS", "1") != "0"
+        # y.  On by default for bf16 only: same-box A/B (profiles/r3_ab_bn_sums.txt) C4 33.50 -> 33.29 ms per step, but
+        # C2 (h3) 52.56 -> 55.07 ms — the h3 weight gradient sits at the 256-VGPR limit of 2 waves / SIMD and the sums'
+        # state costs it more than the cdm_norm_bwd_reduce pass it saves.  $CDM_FUSE_BN_SUMS=0 / 1 forces it.
+        env = os.environ.get("CDM_FUSE_BN_SUMS")
+        self.fuse_bn_sums = self.x16 and (env == "1" if env is not None else not self.h3)
         # init_conv.conv1's BN backward inside its weight-gradient kernel ($CDM_FUSE_CIN1_BWD=0: the apply kernel)
         self.fuse_cin1_bwd = os.environ.get("CDM_FUSE_CIN1_BWD", "1") != "0"
         self.device = torch.device(device)
@@ -890,7 +893,17 @@ def cout1_band_rows(B: int, H: int) -> int:
 
 
 def wgrad_splits(K: int, M: int, N: int) -> int:
-    """Split-K factor for a weight-gradient GEMM: aim for ~2048 workgroups."""
+    """Split-K factor for a weight-gradient GEMM (M = C_out, N = 9 C_in for a 3x3 conv, K = pixels).
+
+    3x3 convs with C_in, C_out % 128 == 0 run the kernel-row weight gradient: 3 (C_out/128) (C_in/128) blocks per split,
+    one 512-thread block per CU at a time, all blocks equal work — so the grid is sized to whole rounds of 256 CUs
+    (768 blocks): 228 splits gave 684 blocks = 2.67 rounds, whose last round ran a third empty (same-box A/B,
+    profiles/r3_ab_wgrad_rounds.txt: C2 train step 53.04 -> 51.89 ms, C4 33.09 -> 32.12 ms).  Others: ~2048
+    workgroups of the generic split GEMM."""
+    if N % 9 == 0 and M % 128 == 0 and (N // 9) % 128 == 0 and os.environ.get("CDM_WGRAD_ROUNDS", "1") != "0":
+        per = 3 * (M // 128) * ((N // 9) // 128)
+        want = max(1, min(512, round(int(os.environ.get("CDM_WGRAD_BLOCKS", "768")) / per)))
+        return lib().raw("cdm_gemm_splits")(K, want)
     tiles = _cdiv(M, 128) * _cdiv(N, 128)
     want = max(1, min(512, _cdiv(2048, tiles)))
     return lib().raw("cdm_gemm_splits")(K, want)

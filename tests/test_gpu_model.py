@@ -270,6 +270,7 @@ def test_fused_bn_fwd_bit_exact_nf128(B):
     import cdm_amd.model as M
     eng = M.get_engine(nf, 6, 64, torch.device("cuda", torch.cuda.current_device()), "h3")
     res = []
+    sums0 = eng.fuse_bn_sums
     eng.fuse_bn_sums = False      # (the producer sums ride on the fused X staging: same sums, other summation order)
     try:
         for fuse in (True, False):
@@ -285,7 +286,7 @@ def test_fused_bn_fwd_bit_exact_nf128(B):
                         {k: v.detach().cpu() for k, v in m.state_dict().items() if "running" in k}))
     finally:
         eng.fuse_bn_fwd = True
-        eng.fuse_bn_sums = True
+        eng.fuse_bn_sums = sums0
         M._WS.clear()
     assert torch.equal(res[0][0], res[1][0])
     for k in res[1][1]:
@@ -297,7 +298,8 @@ def test_fused_bn_fwd_bit_exact_nf128(B):
 @pytest.mark.parametrize("math", ["h3", "bf16"])
 def test_bn_sums_in_consumer_wgrad_nf128(math):
     """The BatchNorm-backward channel sums of each fused dense producer computed in its consumer's weight-gradient X
-    staging (PreBnReluSums, one partial per split) vs the separate cdm_norm_bwd_reduce pass ($CDM_FUSE_BN_SUMS=0), n_feat
+    staging (PreBnReluSums, one partial per block; the bf16 default, on demand under h3) vs the separate
+    cdm_norm_bwd_reduce pass, n_feat
     128, B=3: the forward (eps, running statistics) is untouched (bit-identical); the gradients differ only by the sums'
     fp32 summation order, which moves the BN-backward coefficients by rounding: relative L2 per gradient <= 1e-2 (the
     kink flips of test_train_grads_random_weights_vs_fp64), median <= 1e-4 under h3; under bf16 a last-bit change of
@@ -313,6 +315,7 @@ def test_bn_sums_in_consumer_wgrad_nf128(math):
     import cdm_amd.model as M
     eng = M.get_engine(nf, 6, 64, torch.device("cuda", torch.cuda.current_device()), math)
     res = []
+    sums0 = eng.fuse_bn_sums
     try:
         for on in (True, False):
             eng.fuse_bn_sums = on
@@ -326,7 +329,7 @@ def test_bn_sums_in_consumer_wgrad_nf128(math):
             res.append((pred.detach().cpu(), {k: p.grad.detach().double().cpu() for k, p in m.named_parameters()},
                         {k: v.detach().cpu() for k, v in m.state_dict().items() if "running" in k}))
     finally:
-        eng.fuse_bn_sums = True
+        eng.fuse_bn_sums = sums0
         M._WS.clear()
     assert torch.equal(res[0][0], res[1][0])
     for k in res[1][2]:
