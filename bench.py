@@ -157,9 +157,16 @@ def time_dominant_conv_in_step(trainer, x0, c, rounds: int = 5):
     return ev / (rounds * len(calls)), len(calls)
 
 
+# FETCH_SIZE per byte read in the LDS-halo conv's staging pattern (4 lanes x 16 B = 64 B of a pixel's channel row per
+# chunk): 0.6706, measured on a 537 MB tensor read once in exactly that pattern (tools/fetch_calib.hip,
+# profiles/r3_fetch_calibration.txt); wide 16-B-per-lane streaming reads give the guide's 0.5 (measured 0.5000)
+HALO_FETCH_PER_BYTE = 0.6706
+
+
 def pmc_traffic(math: str):
-    """HBM bytes per launch of the dominant kernel from the committed PMC passes (tools/gpu_profile.sh:
-    FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected), or None when no profile has been collected."""
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes (tools/gpu_profile.sh):
+    FETCH_SIZE / 0.6706 (the halo staging pattern's calibrated counter rate) + WRITE_SIZE (exact for its stores), or
+    None when no profile has been collected."""
     import glob
     suffix = "" if math == "fp32" else "_" + math
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_conv128{suffix}.json")))
@@ -167,7 +174,7 @@ def pmc_traffic(math: str):
         return None
     with open(files[-1]) as f:
         d = json.load(f)
-    return int(d["traffic_bytes"])
+    return int((d["FETCH_SIZE"] / HALO_FETCH_PER_BYTE + d["WRITE_SIZE"]) * 1024)
 
 
 def _cpu_train_rate(R, nf: int, T: int, bs: int, steps: int, warmup: int):

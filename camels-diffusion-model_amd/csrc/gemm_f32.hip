@@ -862,11 +862,16 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     // halo planes padded to HQ x 512 pieces where LDS allows: every piece then has a slot (past-the-halo pieces
     // write unused padding), so the split + store has no branches and can share a scheduling region with MFMAs
     constexpr int HPXA = HQ * HTHREADS / 4;
-    constexpr bool HPAD = (2 * NS * HPXA * XBK + 2 * 3 * NS * XPLANE) * 2 + 7 * 256 * 4 <= 160 * 1024;
+    // ONEB (ABL 2048, one bf16 term only): B of all 9 taps of a chunk in one buffer, one barrier per chunk (36 MFMAs per
+    // wave between barriers instead of 12; the one-term chunk is too short to pay three barrier drains)
+    constexpr bool ONEB = (ABL & 2048) != 0;
+    static_assert(!ONEB || NS == 1, "one barrier per chunk: the one-term images only");
+    constexpr int BGR = ONEB ? 3 : 1;                 // B groups (kernel rows) per buffer
+    constexpr bool HPAD = (2 * NS * HPXA * XBK + 2 * 3 * BGR * NS * XPLANE) * 2 + 7 * 256 * 4 <= 160 * 1024;
     constexpr int HPLANE = (HPAD ? HPXA : HPX) * XBK;   // bf16 per halo term plane
     constexpr int BPL = 3 * NS;                       // B planes per group (3 taps x NS terms)
-    constexpr int BQ = (BPL * 256 + HTHREADS - 1) / HTHREADS;  // 16-byte B pieces per thread
-    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * NS * HPLANE + 2 * BPL * XPLANE];
+    constexpr int BQ = (BGR * BPL * 256 + HTHREADS - 1) / HTHREADS;  // 16-byte B pieces per thread
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * NS * HPLANE + 2 * BGR * BPL * XPLANE];
     __bf16* Hs = smem;                                // [buf][term][halo pixel][16 ch] (xoff swizzle)
     __bf16* Bs = smem + 2 * NS * HPLANE;              // [buf][tap dx][term][col][16 k] (xoff swizzle)
 
@@ -1011,9 +1016,11 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 #pragma unroll
     for (int j = 0; j < BQ; ++j) {
         const int q = tid + j * HTHREADS;
-        const int pl = min(q >> 8, BPL - 1), dx = pl / NS, t = pl - dx * NS, half = q & 1;
+        // ONEB: plane pl = kernel row * BPL + tap (NS == 1); group gr of the chunk at the global group stride
+        const int plg = min(q >> 8, BGR * BPL - 1), gr = plg / BPL, pl = plg - gr * BPL;
+        const int dx = pl / NS, t = pl - dx * NS, half = q & 1;
         const int n = min(n0 + ((q & 255) >> 1), Cout - 1);
-        bpo[j] = (unsigned)(((dx * 3 + t) * Cout + n) * XBK + half * 8) * 2u;
+        bpo[j] = (unsigned)((gr * 9 * Cout + (dx * 3 + t) * Cout + n) * XBK + half * 8) * 2u;
     }
     auto gload_b = [&](int g, u32x4 (&breg)[BQ]) {
         const char* gb = reinterpret_cast<const char*>(wx3) + (long long)g * (9 * XBK * 2) * Cout;
@@ -1033,7 +1040,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 #pragma unroll
         for (int j = 0; j < BQ; ++j) {
             const int q = tid + j * HTHREADS;
-            if (q < BPL * 256)
+            if (q < BGR * BPL * 256)
                 *reinterpret_cast<u32x4*>(base + (q >> 8) * XPLANE + xoff((q & 255) >> 1, (q & 1) * 8)) = breg[j];
         }
     };
@@ -1183,6 +1190,28 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    if constexpr (ONEB) {
+    for (int cc = 0; cc < nchunks; ++cc) {
+        const bool morec = cc + 1 < nchunks;
+        const __bf16* a = Hs + hb * NS * HPLANE;
+        const __bf16* bcur = Bs + bb * 3 * BPL * XPLANE;
+        // the next chunk's 9 taps of B and its halo (or the next tile's first chunk): a whole chunk to arrive
+        gload_b(morec ? (cc + 1) * 3 : 0, bregA);
+        if (!morec && nextt) setup_tile(t + t_step);
+        gload_halo(morec ? cc + 1 : 0);
+        compute(0, a, bcur, V0{});
+        compute(1, a, bcur + BPL * XPLANE, V0{});
+        // staggered (stg): waves 4-7 split + store the next chunk before the last kernel row's MFMAs, waves 0-3 after
+        // them (both buffers idle since the previous chunk's barrier)
+        const bool early = stg && __builtin_amdgcn_readfirstlane(wave) >= 4;   // wave-uniform (scalar branch)
+        if (morec && early) { store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1); store_b((bb ^ 1) * 3 * BPL * XPLANE, bregA); }
+        compute(2, a, bcur + 2 * BPL * XPLANE, V0{});
+        if (morec && !early) { store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1); store_b((bb ^ 1) * 3 * BPL * XPLANE, bregA); }
+        sync();
+        bb ^= 1;
+        hb ^= 1;
+    }
+    } else {
     for (int cc = 0; cc < nchunks; ++cc) {
         const bool morec = cc + 1 < nchunks;
         const int g0 = cc * 3;
@@ -1224,12 +1253,13 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         bb ^= 1;
         hb ^= 1;
     }
+    }
     unscale<NT>(acc, sx, op_scale<NT>(amax_w));
     if (nextt) {   // the next tile's chunk 0 (its loads were issued during the last chunk) into the halo / B buffers
         // idle since the last chunk's closing barrier, ahead of the epilogue: its prefetch registers die before the
         // epilogue and the epilogue needs no barrier pair after it
         store_halo(Hs + hb * NS * HPLANE, 0);
-        store_b(bb * BPL * XPLANE, bregA);
+        store_b(bb * BGR * BPL * XPLANE, bregA);
     }
     // epilogue scratch (stats / max-min: 4 KiB): the other halo buffer (>= 24 KiB), last read by the final chunk
     // before its closing barrier
@@ -1695,6 +1725,12 @@ static int halo_stagger(int nterm) {
     return v >= 0 ? v : (nterm == NT_H3 ? 1 : 0);
 }
 
+// the one-barrier-per-chunk schedule of the one-term (bf16) LDS-halo conv ($CDM_HALO_ONEB=0: three barriers per chunk)
+static int halo_oneb() {
+    static const int v = [] { const char* e = getenv("CDM_HALO_ONEB"); return e ? atoi(e) : 1; }();
+    return v;
+}
+
 template <int WT, class PRE = PreNone>
 static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
                             const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm, hipStream_t s,
@@ -1716,8 +1752,14 @@ static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, cons
         return cdm_status();
     } else {
     switch (nterm) {
-        case 1: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, (1 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
+        case 1:
+            if (halo_oneb())
+                hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, 1 | 2048, PRE>), grid, dim3(HTHREADS),
+                                   0, s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm));
+            else
+                hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, 1, PRE>), grid, dim3(HTHREADS), 0, s,
+                                   x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm));
+            break;
         case 3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<3, WT, EpiStoreW<4>, true, (3 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
                                    Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
         case NT_H3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EpiStoreW<4>, true, (NT_H3 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0,

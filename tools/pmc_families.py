@@ -36,6 +36,8 @@ def main(outdir, subs):
         med = {k: statistics.median(v) for k, v in kv.items()}
         if "FETCH_SIZE" in med:
             med["fetch_bytes_x2"] = med["FETCH_SIZE"] * 2048
+            if "halo" in n:   # the halo staging pattern's calibrated counter rate (profiles/r3_fetch_calibration.txt)
+                med["fetch_bytes_halo_cal"] = med["FETCH_SIZE"] * 1024 / 0.6706
         if "WRITE_SIZE" in med:
             med["write_bytes"] = med["WRITE_SIZE"] * 1024
         w = med.get("SQ_WAVE_CYCLES")

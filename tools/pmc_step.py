@@ -26,6 +26,11 @@ def dispatches(path):
     return [by[k] for k in sorted(by)]
 
 
+# the roofline kernel's instantiation: h3 (4) by default, "conv3x3_halo_x3_kernel<1, 64," for the bf16 C4 step
+KERNEL = os.environ.get("CDM_PMC_KERNEL", "conv3x3_halo_x3_kernel<4, 64,")
+HALO_FETCH_PER_BYTE = 0.6706   # FETCH_SIZE per byte of the halo staging pattern (profiles/r3_fetch_calibration.txt)
+
+
 def roofline_launches(ds):
     steps, cur = [], []
     for d in ds:
@@ -35,7 +40,7 @@ def roofline_launches(ds):
             cur.append(d)
     out = []
     for st in steps[2:]:                       # skip the warm-up / capture steps
-        halo = [d for d in st if "conv3x3_halo_x3_kernel<4, 64," in d["name"]]
+        halo = [d for d in st if KERNEL in d["name"]]
         out.extend(halo[:9])
     return out
 
@@ -52,11 +57,12 @@ def main(outdir):
     d = {"what": "per-launch medians over the roofline conv launches inside the training step", "launches": n,
          "median": med, "algorithmic_bytes": algo}
     if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
-        fb, wb = med["FETCH_SIZE"] * 1024 * 2, med["WRITE_SIZE"] * 1024
+        fb, wb = med["FETCH_SIZE"] * 1024 / HALO_FETCH_PER_BYTE, med["WRITE_SIZE"] * 1024
         d.update(fetch_bytes_corrected=fb, write_bytes=wb, traffic_bytes=fb + wb, traffic_over_algorithmic=(fb + wb) / algo)
     if "SQ_INSTS_MFMA" in med:
         d["mfma_insts"] = med["SQ_INSTS_MFMA"]
-    d["note"] = ("FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes; one counter group per rocprofv3 pass; "
+    d["note"] = ("FETCH_SIZE / 0.6706 (the halo staging pattern's calibrated counter rate, "
+                 "profiles/r3_fetch_calibration.txt), KiB -> bytes; one counter group per rocprofv3 pass; "
                  "algorithmic = x read + y write + weights (fp16 hi/lo) + BN-stat partials")
     print(json.dumps(d, indent=1))
 
