@@ -867,6 +867,11 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     constexpr bool ONEB = (ABL & 2048) != 0;
     static_assert(!ONEB || NS == 1, "one barrier per chunk: the one-term images only");
     constexpr int BGR = ONEB ? 3 : 1;                 // B groups (kernel rows) per buffer
+    // DEEP (ABL 4096, with ONEB, forward staging only): the halo of chunk q+2 is loaded while chunk q computes and
+    // chunk q+1 (loaded one chunk earlier) is stored, so a halo load has two chunks to arrive instead of one (the
+    // one-term chunk is short against HBM latency); two halo register sets, Cin % 32 == 0
+    constexpr bool DEEP = (ABL & 4096) != 0;
+    static_assert(!DEEP || (ONEB && !PRE::on), "two-deep halo prefetch: one-term forward staging only");
     constexpr bool HPAD = (2 * NS * HPXA * XBK + 2 * 3 * BGR * NS * XPLANE) * 2 + 7 * 256 * 4 <= 160 * 1024;
     constexpr int HPLANE = (HPAD ? HPXA : HPX) * XBK;   // bf16 per halo term plane
     constexpr int BPL = 3 * NS;                       // B planes per group (3 taps x NS terms)
@@ -946,6 +951,16 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         hdst[j] = (HPAD || q < HPX * 4) ? xoff(q >> 2, (q & 3) * 4) : -1;
     }
     setup_tile(t_first);
+    // a halo register set and its in-image mask (DEEP: the mask travels with the set across a tile change)
+    auto gload_halo_to = [&](float4 (&dst)[HQ], unsigned& mask, int cc) {
+        const char* xb = reinterpret_cast<const char*>(x + cc * 16);
+        mask = 0u;
+#pragma unroll
+        for (int j = 0; j < HQ; ++j) {
+            dst[j] = *reinterpret_cast<const float4*>(xb + hxo[j]);
+            mask |= (hin[j] ? 1u : 0u) << j;
+        }
+    };
     auto gload_halo = [&](int cc) {
         if constexpr (ABL & 32) {
             if (cc > 0) return;
@@ -959,7 +974,8 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
             for (int j = 0; j < HQ; ++j) yreg[j] = *reinterpret_cast<const float4*>(yb + hyo[j]);
         }
     };
-    auto store_halo = [&](__bf16* base, int cc) {
+    // inb(j): piece j lies inside the image (else zero padding)
+    auto store_halo_impl = [&](const float4 (&src)[HQ], auto inb, __bf16* base, int cc) {
         float cf[NCOEF ? NCOEF : 1][4];   // coefficients of this thread's 4 channels (q & 3 == tid & 3 for every j)
         if constexpr (NCOEF > 0) {
             const int cb = cc * 16 + (tid & 3) * 4;
@@ -972,7 +988,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 #pragma unroll
         for (int j = 0; j < HQ; ++j) {
             if (HPAD || hdst[j] >= 0) {
-                float xv[4] = {hreg[j].x, hreg[j].y, hreg[j].z, hreg[j].w};
+                float xv[4] = {src[j].x, src[j].y, src[j].z, src[j].w};
                 if constexpr (PRE::kind == 1) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
@@ -983,7 +999,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
                     for (int e = 0; e < 4; ++e) xv[e] = bn_relu_elem(xv[e], cf[0][e], cf[1][e]);
                 }
 #pragma unroll
-                for (int e = 0; e < 4; ++e) xv[e] = hin[j] ? xv[e] : 0.f;   // zero padding (transform not applied)
+                for (int e = 0; e < 4; ++e) xv[e] = inb(j) ? xv[e] : 0.f;   // zero padding (transform not applied)
                 __bf16 h[4], m[4], l[4];
                 if constexpr (ABL & 8) {
 #pragma unroll
@@ -1001,6 +1017,10 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
                 if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + 2 * HPLANE) = bf16x4{l[0], l[1], l[2], l[3]};
             }
         }
+    };
+    auto store_halo = [&](__bf16* base, int cc) { store_halo_impl(hreg, [&](int j) { return hin[j]; }, base, cc); };
+    auto store_halo_set = [&](const float4 (&src)[HQ], unsigned mask, __bf16* base, int cc) {
+        store_halo_impl(src, [&](int j) { return ((mask >> j) & 1u) != 0u; }, base, cc);
     };
     // ---- B staging: piece q = (plane q>>8 = dx*NS + t, col (q&255)>>1, k-half q&1) of group g ----
     // two register sets for B: the groups dy = 1 and dy = 2 of a chunk are both fetched at the chunk's start,
@@ -1182,6 +1202,11 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     store_b(0, bregA);
     __syncthreads();
     int hb = 0, bb = 0;
+    // DEEP: set X holds the chunk after the current one (stored at the end of the current chunk), set Y receives the
+    // one after that; the roles alternate per chunk (nchunks is even, so they line up across tiles)
+    float4 hX[DEEP ? HQ : 1], hY[DEEP ? HQ : 1];
+    unsigned mX = 0u, mY = 0u;
+    if constexpr (DEEP) gload_halo_to(hX, mX, 1);
     for (int kt = 0, t = t_first; kt < tpb && t < mtiles; ++kt, t += t_step) {
     const bool nextt = kt + 1 < tpb && t + t_step < mtiles;
 #pragma unroll
@@ -1190,7 +1215,34 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    if constexpr (ONEB) {
+    if constexpr (DEEP) {
+    // chunk cc: B of chunk q+1 and the halo of chunk q+2 are loaded (across the tile end: the next tile's chunks 0 / 1),
+    // the MFMAs of chunk q run, then chunk q+1 (halo from the set loaded one chunk earlier) is stored
+    auto step = [&](int cc, const float4 (&hs)[HQ], unsigned ms, float4 (&hl)[HQ], unsigned& ml) {
+        const bool morec = cc + 1 < nchunks;
+        const bool has1 = morec || nextt;               // chunk q+1 exists in this block
+        const __bf16* a = Hs + hb * NS * HPLANE;
+        const __bf16* bcur = Bs + bb * 3 * BPL * XPLANE;
+        gload_b(morec ? (cc + 1) * 3 : 0, bregA);
+        if (cc + 2 == nchunks && nextt) setup_tile(t + t_step);
+        // chunk q+2: this tile's cc + 2, or the next tile's cc + 2 - nchunks (a dummy reload past the block's end)
+        gload_halo_to(hl, ml, cc + 2 < nchunks ? cc + 2 : cc + 2 - nchunks);
+        compute(0, a, bcur, V0{});
+        compute(1, a, bcur + BPL * XPLANE, V0{});
+        compute(2, a, bcur + 2 * BPL * XPLANE, V0{});
+        if (has1) {
+            store_halo_set(hs, ms, Hs + (hb ^ 1) * NS * HPLANE, morec ? cc + 1 : 0);
+            store_b((bb ^ 1) * 3 * BPL * XPLANE, bregA);
+        }
+        sync();
+        bb ^= 1;
+        hb ^= 1;
+    };
+    for (int cc = 0; cc < nchunks; cc += 2) {
+        step(cc, hX, mX, hY, mY);
+        step(cc + 1, hY, mY, hX, mX);
+    }
+    } else if constexpr (ONEB) {
     for (int cc = 0; cc < nchunks; ++cc) {
         const bool morec = cc + 1 < nchunks;
         const __bf16* a = Hs + hb * NS * HPLANE;
@@ -1255,7 +1307,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     }
     }
     unscale<NT>(acc, sx, op_scale<NT>(amax_w));
-    if (nextt) {   // the next tile's chunk 0 (its loads were issued during the last chunk) into the halo / B buffers
+    if (!DEEP && nextt) {   // the next tile's chunk 0 (its loads were issued during the last chunk) into the halo / B buffers
         // idle since the last chunk's closing barrier, ahead of the epilogue: its prefetch registers die before the
         // epilogue and the epilogue needs no barrier pair after it
         store_halo(Hs + hb * NS * HPLANE, 0);
@@ -1609,15 +1661,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
         for (int t = 0; t < 3; ++t) boff[t][hf] = trswz(kb + 4 * hf + t, cb >> 3) + (cb & 7) * 2;
     }
 
-    if (kt0 < kt1) { gload(); sstore(smem); }
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-        const bool more = kt + 1 < kt1;
-        if (more) gload();
-        const char* a = reinterpret_cast<const char*>(smem + cur * STEP);
+    // the MFMAs of the K step staged in buffer cur_
+    auto mma_at = [&](int cur_) {
+        const char* a = reinterpret_cast<const char*>(smem + cur_ * STEP);
         const char* b = a + NS * IA * 2;
-        auto mma = [&]() {
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
         bf16x8 fa[2][NS];
@@ -1654,7 +1701,14 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
             }
         }
         }
-        };
+    };
+    if (kt0 < kt1) { gload(); sstore(smem); }
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) gload();
+        auto mma = [&]() { mma_at(cur); };
         // stg: the two waves of each SIMD (w, w + 4) run the step in opposite orders — one stages the next K step
         // (VALU: BN transforms, term split, LDS writes) while the other issues its MFMAs, instead of both
         // alternating in lock-step between the barriers
@@ -1731,6 +1785,17 @@ static int halo_oneb() {
     return v;
 }
 
+static int halo_oneb_bwd() {
+    static const int v = [] { const char* e = getenv("CDM_HALO_ONEB_BWD"); return e ? atoi(e) : 0; }();
+    return v;
+}
+
+// the two-chunk-deep halo prefetch of the one-term forward halo conv ($CDM_HALO_DEEP=0: one chunk ahead)
+static int halo_deep() {
+    static const int v = [] { const char* e = getenv("CDM_HALO_DEEP"); return e ? atoi(e) : 1; }();
+    return v;
+}
+
 template <int WT, class PRE = PreNone>
 static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
                             const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm, hipStream_t s,
@@ -1753,7 +1818,16 @@ static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, cons
     } else {
     switch (nterm) {
         case 1:
-            if (halo_oneb())
+            if constexpr (!PRE::on) {
+                if (halo_oneb() && halo_deep() && Cin % 32 == 0) {
+                    hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, 1 | 2048 | 4096, PRE>),
+                                       grid, dim3(HTHREADS), 0, s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre,
+                                       mtiles, tpb, halo_stagger(nterm));
+                    break;
+                }
+            }
+            // (the BN-backward staging form spills 12 VGPRs with the 9-tap B set: one barrier per chunk only by request)
+            if (PRE::on ? halo_oneb_bwd() : halo_oneb())
                 hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, 1 | 2048, PRE>), grid, dim3(HTHREADS),
                                    0, s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm));
             else
@@ -2193,6 +2267,11 @@ static int wgrad_stagger() {
     return v;
 }
 
+// Two staging schedules of this kernel were measured and dropped (bit-identical outputs, same-box A/B,
+// profiles/r3_ab_deep_staging.txt, r3_ab_wgrad_interleave.txt): the K step two ahead loaded into a second register set
+// (BN coefficients moved to LDS to make room): C2 51.07-51.22 -> 51.87-52.01 ms per step, C4 neutral; the same with the
+// next step's staging interleaved into the MFMAs' scheduling region (sched_group_barrier: 1 MFMA, 2 LDS reads, 5 VALU
+// per gap): C2 49.78-49.91 -> 51.19-51.68 ms, C4 neutral.
 template <int KS, class PRE = PreNone, class PX = PreNone>
 static int launch_wgrad_row(const float* dy, int lddy, int Cout, const float* x, int H, int W, int Cin, int ldx, int K,
                             int sp, const float* amax_dy, const float* amax_x, float* slab, int nterm, hipStream_t st,

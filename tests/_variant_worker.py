@@ -1,0 +1,62 @@
+"""Child process of tests/test_gpu_kernels.py::test_deep_staging_bit_exact: runs the bf16 forward halo conv, whose
+staging schedule an environment switch selects ($CDM_HALO_DEEP, read once per process by the library), and the fused
+weight gradients on fixed seeded inputs and saves their outputs, so the test can compare two processes bit for bit.
+
+    python tests/_variant_worker.py OUT.pt
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(out_path):
+    import cdm_amd
+    L = cdm_amd.lib()
+    s = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device="cuda").manual_seed(21)
+    out = {}
+    # one-term forward halo conv with the BN-ReLU staging, several tiles per block and a short last block
+    N, H, C = 97, 64, 128
+    P = N * H * H
+    x = torch.randn(P, C, device="cuda", generator=g)
+    ps, pt = torch.rand(C, device="cuda", generator=g) + 0.5, torch.randn(C, device="cuda", generator=g) * 0.3
+    W = torch.randn(C, C, 3, 3, device="cuda", generator=g) * 0.05
+    b = torch.randn(C, device="cuda", generator=g)
+    wpk = torch.empty(9 * C, C, device="cuda")
+    L.cdm_pack_conv3x3(W.data_ptr(), b.data_ptr(), C, C, None, None, None, None, 0.0, wpk.data_ptr(), None, None, 16, s)
+    wx = torch.empty(9 * C // 16 * 3 * C * 16, dtype=torch.bfloat16, device="cuda")
+    L.cdm_split_bf16x3(wpk.data_ptr(), C, 9 * C, C, wx.data_ptr(), s)
+    y = torch.empty(P, C, device="cuda")
+    st = torch.empty(P // 128, 2, C, device="cuda")
+    assert L.cdm_conv3x3_fwd_x16_ex(x.data_ptr(), N, H, H, C, C, ps.data_ptr(), pt.data_ptr(), wx.data_ptr(), None,
+                                    None, b.data_ptr(), y.data_ptr(), C, C, 0, st.data_ptr(), C, 16, None, None, 0, 1,
+                                    s) == 0
+    out["halo_y"], out["halo_stats"] = y.cpu(), st.cpu()
+    # kernel-row weight gradient, BN-backward dY staging + BN-ReLU X staging, both 16-bit arithmetics
+    from cdm_amd.engine import wgrad_splits
+    for nterm in (4, 1):
+        for (B, S, ci, co) in ((4, 64, 128, 128), (3, 32, 256, 256)):
+            P = B * S * S
+            gy = torch.randn(P, co, device="cuda", generator=g) * 1e-2
+            yy = torch.randn(P, co, device="cuda", generator=g)
+            xx = torch.randn(P, ci, device="cuda", generator=g)
+            cf = [torch.randn(co, device="cuda", generator=g) for _ in range(7)]
+            cf[3] = cf[3].abs() + 0.1
+            xs_, xt_ = torch.rand(ci, device="cuda", generator=g) + 0.5, torch.randn(ci, device="cuda", generator=g)
+            am = torch.ones(2, device="cuda") * 8.0
+            sp = wgrad_splits(P, co, 9 * ci)
+            slab = torch.empty(sp * co * 9 * ci, device="cuda")
+            assert L.cdm_conv3x3_wgrad_x16_ex(gy.data_ptr(), co, yy.data_ptr(), co, *[t.data_ptr() for t in cf], co,
+                                              xx.data_ptr(), B, S, S, ci, ci, xs_.data_ptr(), xt_.data_ptr(), None, 0,
+                                              None, None, None, am.data_ptr(), am.data_ptr() + 4, sp, slab.data_ptr(),
+                                              nterm, s) == 0
+            out[f"wgrad_{nterm}_{S}"] = slab.cpu()
+    torch.cuda.synchronize()
+    torch.save(out, out_path)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -2,6 +2,8 @@
 
 Tolerance: fp32 MFMA vs CPU fp32 with different summation order -> |err| <= 2e-5 * max|ref| + 1e-5.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -408,6 +410,66 @@ def test_bn_bwd_fused_into_conv_staging_bit_exact(L, N, S, C, Cin):
                                  amx.data_ptr(), sp, s_got.data_ptr(), _s())
     torch.cuda.synchronize()
     assert torch.equal(s_got, s_ref)
+
+
+@pytest.mark.parametrize("N,H,Cin,pre", [(97, 64, 128, False), (66, 64, 128, True), (40, 32, 256, True),
+                                         (2, 64, 128, False)])
+def test_bf16_halo_conv_vs_fp64(L, N, H, Cin, pre):
+    """The one-term (bf16, C4) LDS-halo forward — one barrier per chunk, halo prefetched two chunks ahead, several
+    256-pixel tiles per block incl. a short last block (N=97: 1,552 tiles, 3 per block) — against an fp64 conv of the
+    same bf16-rounded operands: only fp32 accumulation error may remain (<= 5e-6 max|ref|), with the BN-ReLU staging
+    of the fused forward (pre: z = relu(y s + t) rounded to bf16) and the batch-statistics epilogue."""
+    Cout = 128
+    g_ = torch.Generator(device="cuda").manual_seed(13)
+    P = N * H * H
+    x = torch.randn(P, Cin, device="cuda", generator=g_)
+    s_ = torch.rand(Cin, device="cuda", generator=g_) + 0.5
+    t_ = torch.randn(Cin, device="cuda", generator=g_) * 0.3
+    W = torch.randn(Cout, Cin, 3, 3, device="cuda", generator=g_) * 0.05
+    b = torch.randn(Cout, device="cuda", generator=g_)
+    wpk, _ = _pack3x3(L, W, b, 16)
+    wx = _split(L, wpk, 9 * Cin, Cout)
+    y = torch.full((P, Cout), float("nan"), device="cuda")
+    stats = torch.zeros(P // 128, 2, Cout, device="cuda")
+    assert L.cdm_conv3x3_fwd_x16_ex(x.data_ptr(), N, H, H, Cin, Cin, s_.data_ptr() if pre else None,
+                                    t_.data_ptr() if pre else None, wx.data_ptr(), None, None, b.data_ptr(),
+                                    y.data_ptr(), Cout, Cout, 0, stats.data_ptr(), Cout, 16, None, None, 0, 1,
+                                    _s()) == 0
+    torch.cuda.synchronize()
+    xin = x.double()
+    if pre:
+        xin = (xin * s_.double() + t_.double()).float().double().relu()
+    xb = xin.float().bfloat16().double().cpu().reshape(N, H, H, Cin).permute(0, 3, 1, 2)
+    Wb = W.bfloat16().double().cpu()
+    ref = F.conv2d(xb, Wb, b.double().cpu(), padding=1).permute(0, 2, 3, 1).reshape(P, Cout)
+    got = y.double().cpu()
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert err <= 5e-6, err
+    st = stats.double().cpu().sum(0)
+    assert ((st[0] - ref.sum(0)).abs() <= 1e-5 * ref.abs().sum(0)).all()
+    assert ((st[1] - (ref * ref).sum(0)).abs() <= 1e-5 * (ref * ref).sum(0)).all()
+
+
+def test_deep_staging_bit_exact(L, tmp_path):
+    """The two-deep staging schedule of the bf16 forward halo conv (the halo two chunks ahead, $CDM_HALO_DEEP) produces
+    the one-ahead schedule's output bit for bit, and the fused weight gradients are reproducible across processes: the
+    same kernels in two child processes (tests/_variant_worker.py), the library reading the switch once per process."""
+    import subprocess
+    import sys
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_variant_worker.py")
+    outs = []
+    for deep in ("1", "0"):
+        f = tmp_path / f"deep{deep}.pt"
+        env = dict(os.environ, CDM_HALO_DEEP=deep)
+        r = subprocess.run([sys.executable, worker, str(f)], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(torch.load(f))
+    a, b = outs
+    assert a.keys() == b.keys()
+    for k in a:
+        assert torch.isfinite(a[k]).all(), k
+        assert torch.equal(a[k], b[k]), k
 
 
 @pytest.mark.gpu
