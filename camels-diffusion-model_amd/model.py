@@ -15,6 +15,8 @@ used by the captured train/sample loops).
 """
 from __future__ import annotations
 
+import itertools
+
 import os
 from typing import Dict, List, Optional
 
@@ -105,6 +107,7 @@ class EmbedFC(_Holder):
 # engine registry / autograd bridge
 # ------------------------------------------------------------------------------------------------
 _ENGINES: Dict[tuple, UNetEngine] = {}
+_MODEL_UIDS = itertools.count()
 
 
 def get_engine(n_feat, n_cfeat, height, device, conv_math: str = "fp32") -> UNetEngine:
@@ -196,6 +199,7 @@ class ContextUnet(nn.Module):
             raise ValueError("shortcut_source must be 'cpu' or 'device'")
         self.shortcut_source = shortcut_source
         self._param_names: List[str] = [n for n, _ in self.named_parameters()]
+        self._uid = next(_MODEL_UIDS)     # eval-pack cache identity (see _eval_pack_key)
         self._eval_key = None
         self._sc_counter = 0
 
@@ -219,7 +223,10 @@ class ContextUnet(nn.Module):
         self._eval_key = None
 
     def _eval_pack_key(self, P):
-        return tuple((v.data_ptr(), v._version) for v in P.values())
+        # the engine (and its packed eval weights) is shared by every model of one shape: the key names this model, not
+        # only its tensors' addresses and versions — a model built after another was freed can receive the same
+        # addresses with the same version counters, and would then run on the freed model's stale pack
+        return (self._uid,) + tuple((v.data_ptr(), v._version) for v in P.values())
 
     def draw_shortcut(self, device, n_sets: int = 1):
         """Fresh 1x1 shortcut (diffusion_utilities.py:54).  Returns (w [n_sets*nf], b [n_sets*nf])."""

@@ -344,3 +344,25 @@ def test_bn_sums_in_consumer_wgrad_nf128(math):
         assert max(errs) <= 1e-2 and float(np.median(errs)) <= 1e-4
     else:
         assert max(errs) <= 5e-2 and float(np.median(errs)) <= 5e-3
+
+
+def test_eval_pack_not_shared_across_models():
+    """Models of one shape share an engine and its packed eval weights; a model created after another was freed can
+    get the freed model's tensor addresses with the same version counters.  Its eval forward must still run on its own
+    weights (the pack key carries the model's identity): ten models of different seeds, each freed before the next
+    is built, each eval forward vs the oracle on that model's weights."""
+    import gc
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(2, 1, 64, 64, generator=g); t = torch.rand(2, generator=g); c = torch.rand(2, 6, generator=g)
+    for seed in range(10):
+        m = _model(16, seed=100 + seed, math="h3").eval()
+        sd = R.clone_sd(m.state_dict())
+        with torch.no_grad():
+            torch.manual_seed(5)
+            eps = m(x.cuda(), t.cuda(), c.cuda())
+        torch.manual_seed(5)
+        ref = R.unet_forward(sd, x, t, c, n_feat=16, n_cfeat=6, height=64, train=False,
+                             shortcut=lambda: R.draw_shortcut(1, 16))
+        assert _rel(eps, ref) < 2e-4, seed
+        del m, eps
+        gc.collect()
