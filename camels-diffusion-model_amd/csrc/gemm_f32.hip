@@ -1767,8 +1767,11 @@ static int halo_tpb(int mtiles, int ntiles, int nterm, int wt) {
     (void)nterm; (void)wt;
     static const int forced = [] { const char* e = getenv("CDM_HALO_TPB"); return e ? atoi(e) : 0; }();
     if (forced > 0) return forced;   // A/B timing override (tools), never set by the product
-    const int t = (mtiles * ntiles) / 512;
-    return t < 1 ? 1 : (t > 8 ? 8 : t);
+    // $CDM_HALO_BLOCKS: the block count the tiles are dealt to (512 = two rounds of one block per CU; 256 = one)
+    static const int blocks = [] { const char* e = getenv("CDM_HALO_BLOCKS"); return e ? atoi(e) : 512; }();
+    const int maxt = blocks <= 256 ? 16 : 8;
+    const int t = (mtiles * ntiles) / (blocks > 0 ? blocks : 512);
+    return t < 1 ? 1 : (t > maxt ? maxt : t);
 }
 
 // the staggered halo split of the LDS-halo conv: on for h3, off for the one-term bf16 images ($CDM_HALO_STAGGER=0 / 1
