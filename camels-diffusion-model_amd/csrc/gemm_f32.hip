@@ -1758,7 +1758,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
     }
 }
 
-// tiles per block of the LDS-halo conv: as many as keep >= 512 blocks (2 per CU), at most 8.  Kernel level
+// tiles per block of the LDS-halo conv (round 3: one round of 256 blocks, up to 16 tiles; round 2: >= 512 blocks, at most 8).  Kernel level
 // (tools/conv_ablation.py, h3 128->128 @64^2, B=256, one box): 1 tile 0.872 ms, 2: 0.854, 4: 0.848, 8: 0.843,
 // 16: 0.834.  Bench, same box, 2 runs each (tpb 1 -> this policy): C2 train 4296 -> 4355 img/s, sampling 15.94 ->
 // 15.71 ms per step (CFG 31.95 -> 31.50), C4 bf16 train 6416 -> 6478, sample 9.69 -> 9.46 ms, C5 train 70.7 ->
@@ -1767,8 +1767,10 @@ static int halo_tpb(int mtiles, int ntiles, int nterm, int wt) {
     (void)nterm; (void)wt;
     static const int forced = [] { const char* e = getenv("CDM_HALO_TPB"); return e ? atoi(e) : 0; }();
     if (forced > 0) return forced;   // A/B timing override (tools), never set by the product
-    // $CDM_HALO_BLOCKS: the block count the tiles are dealt to (512 = two rounds of one block per CU; 256 = one)
-    static const int blocks = [] { const char* e = getenv("CDM_HALO_BLOCKS"); return e ? atoi(e) : 512; }();
+    // the block count the tiles are dealt to: 256 = one round of one block per CU (up to 16 tiles per block).  Same-box
+    // A/B, 2 rounds (profiles/r3_ab_grid_blocks.txt): vs 512 (two rounds, up to 8 tiles) C2 train step 51.32 -> 51.13 ms,
+    // C4 31.82 -> 31.70 ms ($CDM_HALO_BLOCKS overrides)
+    static const int blocks = [] { const char* e = getenv("CDM_HALO_BLOCKS"); return e ? atoi(e) : 256; }();
     const int maxt = blocks <= 256 ? 16 : 8;
     const int t = (mtiles * ntiles) / (blocks > 0 ? blocks : 512);
     return t < 1 ? 1 : (t > maxt ? maxt : t);

@@ -1,6 +1,6 @@
 # round-3 validation at HEAD: full GPU suite, smoke, default bench line
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
-timeout -k 10 120 python -u tools/lik_debug.py 2>&1 | grep -v amdgpu.ids
+
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r3_gputests_b.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r3_gputests_b.log; exit 1; }
 tail -2 gpurun_out/r3_gputests_b.log
 timeout -k 10 90 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3_smoke_b.log 2>&1 || { cat gpurun_out/r3_smoke_b.log; exit 1; }
