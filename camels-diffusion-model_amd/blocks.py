@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from ._lib import Mlp4, lib
-from .engine import APPLY_POOL, APPLY_RELU, APPLY_RESID, CHUNK, EPI_RELU, _cdiv, conv_kc, fold, wgrad_splits
+from .engine import APPLY_POOL, APPLY_RELU, APPLY_RESID, CHUNK, EPI_ACCUM, EPI_RELU, _cdiv, conv_kc, fold, wgrad_splits
 
 
 def _p(t):
@@ -261,19 +261,57 @@ def conv_bn_relu(seq: nn.Sequential, xh: torch.Tensor, B: int, H: int, W: int, p
 
 def residual_block(blk, xh: torch.Tensor, x_nchw: torch.Tensor, B: int, H: int, W: int, pool: bool = False,
                    tape: "_Tape" = None):
-    """ResidualConvBlock.forward (diffusion_utilities.py:39-65) on NHWC xh."""
-    resid = None
-    if blk.is_res:
-        Cin, Cout = blk.conv1[0].in_channels, blk.conv2[0].out_channels
-        if blk.same_channels or Cin != 1:
-            raise NotImplementedError("the HIP block path implements the reference's is_res shortcut for in_channels=1 "
-                                      "(ContextUnet's init_conv); same-channel / wider residual adds are not built")
+    """ResidualConvBlock.forward (diffusion_utilities.py:39-65) on NHWC xh.  is_res: out = x + x2 (same channels) or
+    shortcut(x) + x2, the shortcut a fresh nn.Conv2d(Cin, Cout, 1) drawn from the CPU RNG on every call (:54) — C_in = 1
+    inside the conv2 apply (ContextUnet's init_conv), C_in > 1 as a GEMM accumulated onto the output."""
+    if not blk.is_res:
+        z1 = conv_bn_relu(blk.conv1, xh, B, H, W, tape=tape)
+        return conv_bn_relu(blk.conv2, z1, B, H, W, pool=pool, resid=None, tape=tape)
+    Cin, Cout = blk.conv1[0].in_channels, blk.conv2[0].out_channels
+    if pool:
+        raise NotImplementedError("a residual block with the fused MaxPool2d (the reference's UnetDown blocks are not "
+                                  "residual)")
+    if not blk.same_channels:
         # the reference draws a fresh 1x1 conv on every call (diffusion_utilities.py:54): same CPU RNG consumption
         sc = nn.Conv2d(Cin, Cout, kernel_size=1, stride=1, padding=0)
-        resid = (x_nchw.reshape(-1).contiguous(), sc.weight.detach().reshape(Cout).to(xh.device),
-                 sc.bias.detach().to(xh.device))
-    z1 = conv_bn_relu(blk.conv1, xh, B, H, W, tape=tape)
-    return conv_bn_relu(blk.conv2, z1, B, H, W, pool=pool, resid=resid, tape=tape)
+        sw, sb = sc.weight.detach().reshape(Cout, Cin).to(xh.device), sc.bias.detach().to(xh.device)
+        if Cin == 1:
+            resid = (x_nchw.reshape(-1).contiguous(), sw.reshape(Cout).contiguous(), sb)
+            z1 = conv_bn_relu(blk.conv1, xh, B, H, W, tape=tape)
+            return conv_bn_relu(blk.conv2, z1, B, H, W, resid=resid, tape=tape)
+        if Cin % 4 or Cout % 4:
+            raise NotImplementedError("the HIP residual shortcut GEMM needs channels % 4 == 0")
+    L, s = lib(), _s()
+    P = B * H * W
+    sub = None
+    if tape is not None:        # the block's two layers on a tape of their own; the skip joins in one parent op
+        sub = _Tape()
+        sub.grads = tape.grads
+    first = tape is not None and not tape.ops
+    z1 = conv_bn_relu(blk.conv1, xh, B, H, W, tape=sub)
+    out = conv_bn_relu(blk.conv2, z1, B, H, W, tape=sub)
+    if blk.same_channels:       # out += x
+        L.cdm_slab_reduce(xh.data_ptr(), 1, P, Cout, out.data_ptr(), Cout, 0, 1, Cout, 1, 1.0, s)
+    else:                       # out += x . W^T + b
+        swT = torch.empty(Cin, Cout, device=xh.device)
+        L.cdm_transpose(sw.contiguous().data_ptr(), Cout, Cin, swT.data_ptr(), s)
+        if L.cdm_gemm_f32(xh.data_ptr(), Cin, P, Cin, swT.data_ptr(), Cout, Cout, out.data_ptr(), Cout, sb.data_ptr(),
+                          Cout, EPI_ACCUM, 1, None, s):
+            raise RuntimeError("cdm_gemm_f32 (residual shortcut) failed")
+    if tape is not None:
+        def op(g):
+            sub.need_input = tape.need_input if first else True
+            dx = sub.run(g)
+            if dx is None:
+                return None
+            if blk.same_channels:   # dx += g
+                L.cdm_slab_reduce(g.data_ptr(), 1, P, Cout, dx.data_ptr(), Cin, 0, 1, Cout, 1, 1.0, _s())
+            elif L.cdm_gemm_f32(g.data_ptr(), Cout, P, Cout, sw.contiguous().data_ptr(), Cin, Cin, dx.data_ptr(), Cin,
+                                None, 1, EPI_ACCUM, 1, None, _s()):   # dx += g . W
+                raise RuntimeError("cdm_gemm_f32 (residual shortcut backward) failed")
+            return dx
+        tape.ops.append(op)
+    return out
 
 
 def _new_tape(module: nn.Module, *inputs):

@@ -194,3 +194,35 @@ def test_eval_block_backward_raises():
     out = gpu(torch.randn(2, 16, 8, 8, device="cuda"))
     with pytest.raises(NotImplementedError):
         out.sum().backward()
+
+
+@pytest.mark.parametrize("cin,cout", [(32, 32), (16, 32)])
+def test_residual_block_is_res_same_and_wide(cin, cout):
+    """is_res blocks beyond ContextUnet's C_in = 1 form (diffusion_utilities.py:39-65): same channels out = x + x2,
+    wider out = shortcut(x) + x2 with the fresh CPU-RNG 1x1 shortcut of every call; forward and the train-mode backward
+    (parameters and input) vs torch autograd on the CPU."""
+    from cdm_amd import ResidualConvBlock
+    torch.manual_seed(15)
+    cpu = ResidualConvBlock(cin, cout, is_res=True)
+    gpu = copy.deepcopy(cpu).cuda()
+    g = torch.Generator().manual_seed(16)
+    x = torch.randn(2, cin, 16, 16, generator=g)
+    w = torch.randn(2, cout, 16, 16, generator=g)
+    xc = x.clone().requires_grad_(True)
+    torch.manual_seed(7)
+    x2 = _rcb_ref(cpu, xc)
+    ref = xc + x2 if cin == cout else torch.nn.Conv2d(cin, cout, 1)(xc) + x2
+    (ref * w).sum().backward()
+    xg = x.cuda().requires_grad_(True)
+    torch.manual_seed(7)
+    got = gpu(xg)
+    assert _rel(got, ref) < 1e-4
+    (got * w.cuda()).sum().backward()
+    refp = dict(cpu.named_parameters())
+    for n, p in gpu.named_parameters():
+        if n.endswith("0.bias"):
+            continue
+        e = ((p.grad.cpu() - refp[n].grad).norm() / refp[n].grad.norm()).item()
+        assert e < 1e-4, (n, e)
+    e = ((xg.grad.cpu() - xc.grad).norm() / xc.grad.norm()).item()
+    assert e < 1e-4, e
