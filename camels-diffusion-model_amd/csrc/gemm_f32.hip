@@ -185,7 +185,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
     int ymm_ld = 0;              //   ymm[n] (atomic max), ymm[ymm_ld + n] (atomic min); needs stats
     __device__ __forceinline__ void operator()(f32x16 (&acc)[2][2], int mw, int nw, int lane, int wm, int wn,
                                                float* scratch, int tid) const {
-        float* yz = y + (long long)blockIdx.z * zstride;
+        float* yz = y + (long long)blockIdx.z * zstride;   // 0 when the kernel applied its own (remapped) slab
         float cs[2] = {0.f, 0.f}, cq[2] = {0.f, 0.f};
         float cmx[2] = {-INFINITY, -INFINITY}, cmn[2] = {INFINITY, INFINITY};
         float am = 0.f;
@@ -237,7 +237,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
         __syncthreads();
         if (tid < GBN * (WM / 2)) {   // tile t of the block's WM/2 128-row tiles sums waves 2t and 2t+1
             const int t = tid / GBN, c = tid - t * GBN;
-            const int n = blockIdx.y * GBN + c;
+            const int n = (nw - wn * 64) + c;
             if (n < N) {
                 float* st = stats + (long long)((mw - wm * 64) / GBM + t) * 2 * stats_ld;
                 st[n] = scratch[(4 * t + 0) * GBN + c] + scratch[(4 * t + 2) * GBN + c];
@@ -262,7 +262,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
         }
         __syncthreads();
         if (tid < GBN) {
-            const int n = blockIdx.y * GBN + tid;
+            const int n = (nw - wn * 64) + tid;
             if (n < N) {
                 float mx = scratch[tid], mn = scratch[WM * GBN + tid];
 #pragma unroll
@@ -277,6 +277,8 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
     }
 };
 using EpiStore = EpiStoreW<2>;
+template <class EP> struct IsEpiStoreW : std::false_type {};
+template <int WM> struct IsEpiStoreW<EpiStoreW<WM>> : std::true_type {};
 
 struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n, 2h+i, 2w+j, co] = acc + b[co]
     float* y; long long ldy; const float* bias; int H, W, Co, M, N;
@@ -656,8 +658,16 @@ struct StageColK {
 // SA: operand A stager (rows = M), SB: operand B stager (rows = N); split-K over blockIdx.z.  KS 16-deep K
 // tiles share one barrier interval (one stager copy per tile; tiles past the split's end are zero-filled).
 // (KS = 2 measured: ConvT 2x2 fwd 602 -> 695 us, 64 KiB LDS costs a block per CU — KS = 1 ships)
-template <class SA, class SB, class EP, int NT, bool XCD_REMAP, int KS = 1>
-__global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa0, SB sb0, EP ep, int K, int kt_per_split) {
+// order == 1 (operand-sharing block order): the flat block id, dealt round-robin over the 8 XCDs by the dispatcher,
+// is remapped XCD-contiguous and decomposed column-tile fastest, then row tile, then K split, so the blocks that
+// read the same A rows (and, split-K, the same K range of B) run together on one XCD and share its L2: with the
+// grid's natural order (column tile = blockIdx.y, dispatched after every row tile) A was re-read from HBM once per
+// column tile.  order == 0: XCD_REMAP of the row tile only (the previous schedule).
+// MINB: the launch-bounds minimum of resident blocks (2: the compiler settles at 3 waves per SIMD, 155 VGPRs; 4: 4
+// waves per SIMD, <= 128 VGPRs — the ConvT forward fits without spills).
+template <class SA, class SB, class EP, int NT, bool XCD_REMAP, int KS = 1, int MINB = 2>
+__global__ __launch_bounds__(GTHREADS, MINB) void gemm_x3_kernel(SA sa0, SB sb0, EP ep, int K, int kt_per_split,
+                                                              int order) {
     constexpr int NS = XTerms<NT>::NS;
     constexpr int TILE = NS * XPLANE;                 // bf16 per operand per K tile
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * KS * TILE];
@@ -666,14 +676,20 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa0, SB sb0, EP
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    int bx = blockIdx.x;
-    if constexpr (XCD_REMAP) {
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (order == 1) {
+        const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy * gridDim.z;
+        const int L = bx + gx * (by + gy * bz), q = nwg >> 3, r = nwg & 7, xcd = L & 7, j = L >> 3;
+        int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+        by = l % gy; l /= gy;
+        bx = l % gx; bz = l / gx;
+    } else if constexpr (XCD_REMAP) {
         const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = bx & 7, j = bx >> 3;
         bx = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
     }
-    const int m0 = bx * GBM, n0 = blockIdx.y * GBN;
+    const int m0 = bx * GBM, n0 = by * GBN;
     const int ktiles = (K + XBK - 1) / XBK;
-    const int kt0 = blockIdx.z * kt_per_split;
+    const int kt0 = bz * kt_per_split;
     const int kt1 = min(ktiles, kt0 + kt_per_split);
 
     f32x16 acc[2][2];
@@ -749,7 +765,19 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x3_kernel(SA sa0, SB sb0, EP
         cur ^= 1;
     }
     unscale<NT>(acc, sa0.sc_of(), sb0.sc_of());
-    ep(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
+    EP e = ep;
+    if constexpr (IsEpiStoreW<EP>::value) { e.y += (long long)bz * e.zstride; e.zstride = 0; }   // this split's slab
+    e(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
+}
+
+static int gemm_minb() {    // $CDM_GEMM_MINB: 4 (the default) or 2 resident blocks per CU asked of the compiler
+    static const int v = [] { const char* e = getenv("CDM_GEMM_MINB"); return e ? atoi(e) : 4; }();
+    return v;
+}
+
+static int gemm_order() {   // $CDM_GEMM_ORDER: 1 operand-sharing block order (default), 0 grid order
+    static const int v = [] { const char* e = getenv("CDM_GEMM_ORDER"); return e ? atoi(e) : 1; }();
+    return v;
 }
 
 // SA<NS>/SB<NS> are stager templates; splits as launch_gemm (K-tile ranges over blockIdx.z)
@@ -762,16 +790,30 @@ static int launch_gemm_x3(MkA mka, MkB mkb, const EP& ep, int M, int N, int K, i
     const int per = (ktiles + splits - 1) / splits;
     splits = ktiles > 0 ? (ktiles + per - 1) / per : 1;
     dim3 grid((M + GBM - 1) / GBM, (N + GBN - 1) / GBN, splits);
+    const int order = gemm_order();
     switch (nterm) {
-        case 1: hipLaunchKernelGGL((gemm_x3_kernel<SAT<1>, SBT<1>, EP, 1, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
-                                   mka.template make<1>(), mkb.template make<1>(), ep, K, per); break;
+        case 1:
+            if (gemm_minb() == 4)
+                hipLaunchKernelGGL((gemm_x3_kernel<SAT<1>, SBT<1>, EP, 1, XCD_REMAP, 1, 4>), grid, dim3(GTHREADS), 0, s,
+                                   mka.template make<1>(), mkb.template make<1>(), ep, K, per, order);
+            else
+                hipLaunchKernelGGL((gemm_x3_kernel<SAT<1>, SBT<1>, EP, 1, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
+                                   mka.template make<1>(), mkb.template make<1>(), ep, K, per, order);
+            break;
         case 3: hipLaunchKernelGGL((gemm_x3_kernel<SAT<3>, SBT<3>, EP, 3, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
-                                   mka.template make<3>(), mkb.template make<3>(), ep, K, per); break;
-        case NT_H3: hipLaunchKernelGGL((gemm_x3_kernel<SAT<NT_H3>, SBT<NT_H3>, EP, NT_H3, XCD_REMAP>), grid,
-                                       dim3(GTHREADS), 0, s, mka.template make<NT_H3>(), mkb.template make<NT_H3>(), ep,
-                                       K, per); break;
+                                   mka.template make<3>(), mkb.template make<3>(), ep, K, per, order); break;
+        case NT_H3:
+            if (gemm_minb() == 4)
+                hipLaunchKernelGGL((gemm_x3_kernel<SAT<NT_H3>, SBT<NT_H3>, EP, NT_H3, XCD_REMAP, 1, 4>), grid,
+                                   dim3(GTHREADS), 0, s, mka.template make<NT_H3>(), mkb.template make<NT_H3>(), ep, K,
+                                   per, order);
+            else
+                hipLaunchKernelGGL((gemm_x3_kernel<SAT<NT_H3>, SBT<NT_H3>, EP, NT_H3, XCD_REMAP>), grid,
+                                   dim3(GTHREADS), 0, s, mka.template make<NT_H3>(), mkb.template make<NT_H3>(), ep, K,
+                                   per, order);
+            break;
         case 6: hipLaunchKernelGGL((gemm_x3_kernel<SAT<6>, SBT<6>, EP, 6, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
-                                   mka.template make<6>(), mkb.template make<6>(), ep, K, per); break;
+                                   mka.template make<6>(), mkb.template make<6>(), ep, K, per, order); break;
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();
