@@ -157,8 +157,18 @@ __global__ __launch_bounds__(256) void slab_colsum_kernel(const float* __restric
     const int t0 = blockIdx.y * per, t1 = min(ntiles, t0 + per);
     for (int r = 0; r < R; ++r) {
         double acc = 0.0;
-        if (c < C)
-            for (int t = t0 + lane; t < t1; t += 4) acc += (double)slab[((long long)t * R + r) * C + c];
+        if (c < C) {
+            // the same serial order of additions, its loads issued 8 at a time (the loop was load-latency bound)
+            int t = t0 + lane;
+            for (; t + 28 < t1; t += 32) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = slab[((long long)(t + 4 * u) * R + r) * C + c];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc += (double)v[u];
+            }
+            for (; t < t1; t += 4) acc += (double)slab[((long long)t * R + r) * C + c];
+        }
         red[lane][cl] = acc;
         __syncthreads();
         if (lane == 0 && c < C)
