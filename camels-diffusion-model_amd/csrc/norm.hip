@@ -193,11 +193,23 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* part
     if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
     {
         double s = 0.0, q = 0.0;
-        if (c < C)
-            for (int t = ln; t < S; t += 16) {
+        if (c < C) {
+            int t = ln;
+            for (; t + 48 < S; t += 64) {   // loads 4 partials ahead, additions in the serial order
+                double vs[4], vq[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    vs[u] = part[((long long)(t + 16 * u) * R + 0) * C + c];
+                    vq[u] = part[((long long)(t + 16 * u) * R + 1) * C + c];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) { s += vs[u]; q += vq[u]; }
+            }
+            for (; t < S; t += 16) {
                 s += part[((long long)t * R + 0) * C + c];
                 q += part[((long long)t * R + 1) * C + c];
             }
+        }
         rs[ln][cl] = s; rq[ln][cl] = q;
     }
     __syncthreads();
@@ -282,11 +294,23 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* part
     const int c = blockIdx.x * 16 + cl;
     {
         double s1 = 0.0, s2 = 0.0, s5 = 0.0;
-        if (c < C)
-            for (int t = ln; t < S; t += 16) {
+        if (c < C) {
+            int t = ln;
+            for (; t + 48 < S; t += 64) {   // loads 4 partials ahead, additions in the serial order
+                double v1[4], v2[4], v5[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double* p = part + (long long)(t + 16 * u) * 5 * C;
+                    v1[u] = p[0 * C + c]; v2[u] = p[1 * C + c]; v5[u] = p[4 * C + c];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) { s1 += v1[u]; s2 += v2[u]; s5 += v5[u]; }
+            }
+            for (; t < S; t += 16) {
                 const double* p = part + (long long)t * 5 * C;
                 s1 += p[0 * C + c]; s2 += p[1 * C + c]; s5 += p[4 * C + c];
             }
+        }
         r1[ln][cl] = s1; r2[ln][cl] = s2; r5[ln][cl] = s5;
     }
     __syncthreads();
