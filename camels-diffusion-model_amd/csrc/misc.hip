@@ -145,6 +145,54 @@ __global__ __launch_bounds__(256) void conv_cin1_fwd_kernel(const float* x, int 
     if (amax) block_amax_commit(am, amax);
 }
 
+// Row form of conv_cin1_fwd_kernel (and, below, of conv_cout1_dgrad_kernel): a block owns one image row (n, h), its
+// three source rows (zero-padded, W + 2 wide) staged once in LDS, lanes over channel quads and pixels of the row.  The
+// flat-pixel kernels spend a 64-bit division and nine bounds-checked global loads per pixel and lane and write at
+// ~2.8 TB/s; here the output row is a plain coalesced stream.  The same fmaf sequence over the taps (zeros where the
+// image ends, as there): bit-identical results.  W <= ROWK_MAXW (the flat kernels serve wider maps).
+constexpr int ROWK_MAXW = 2048;
+__global__ __launch_bounds__(256) void conv_cin1_fwd_row_kernel(const float* __restrict__ x, int H, int W,
+                                                                const float* __restrict__ w9,
+                                                                const float* __restrict__ bias, float* __restrict__ y,
+                                                                int ldy, int C, int relu, float* amax) {
+    extern __shared__ float xs[];   // [3][W + 2]
+    const int n = blockIdx.x / H, h = blockIdx.x - n * H, WP = W + 2;
+    for (int i = threadIdx.x; i < 3 * WP; i += 256) {
+        const int r = i / WP, col = i - r * WP, hh = h + r - 1, ww = col - 1;
+        xs[i] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? x[((long long)n * H + hh) * W + ww] : 0.f;
+    }
+    const int C4 = C >> 2, PP = 256 / C4;
+    const int c4 = (threadIdx.x % C4) * 4, pl = threadIdx.x / C4;
+    const bool active = pl < PP;
+    float wr[9][4], bb[4];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wr[tap][j] = active ? w9[tap * C + c4 + j] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bb[j] = active ? bias[c4 + j] : 0.f;
+    __syncthreads();
+    float am = 0.f;
+    float* yr = y + ((long long)n * H + h) * W * ldy;
+    for (int w = active ? pl : W; w < W; w += PP) {
+        float o[4] = {bb[0], bb[1], bb[2], bb[3]};
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const float xv = xs[(tap / 3) * WP + w + tap % 3];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = fmaf(xv, wr[tap][j], o[j]);
+        }
+        if (relu) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = relu_f(o[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) am = fmaxf(am, fabsf(o[j]));
+        st4(yr + (long long)w * ldy + c4, make_float4(o[0], o[1], o[2], o[3]));
+    }
+    if (amax) block_amax_commit(am, amax);
+}
+
 // BN backward of the init conv's Conv -> BatchNorm -> ReLU applied while reading its dy (FUSED): dy is never written
 struct Cin1BnBwd { const float* y; int ldy; const float* p[7]; };   // s, t, mean, invstd, A, B, Cc
 
@@ -402,6 +450,39 @@ __global__ __launch_bounds__(256) void conv_cout1_dgrad_kernel(const float* deps
                 for (int j = 0; j < 4; ++j) o[j] = fmaf(gv[u][tap], wr[tap][j], o[j]);
             st4(dz + pix * lddz + c4, make_float4(o[0], o[1], o[2], o[3]));
         }
+    }
+}
+
+// row form of conv_cout1_dgrad_kernel (as conv_cin1_fwd_row_kernel): deps rows h+1, h, h-1 of image n in LDS
+__global__ __launch_bounds__(256) void conv_cout1_dgrad_row_kernel(const float* __restrict__ deps, int H, int W, int C,
+                                                                   const float* __restrict__ w, float* __restrict__ dz,
+                                                                   int lddz) {
+    extern __shared__ float gs[];   // [3][W + 2]: gs[r][col] = deps[h + 1 - r][col - 1]
+    const int n = blockIdx.x / H, h = blockIdx.x - n * H, WP = W + 2;
+    for (int i = threadIdx.x; i < 3 * WP; i += 256) {
+        const int r = i / WP, col = i - r * WP, hh = h + 1 - r, ww = col - 1;
+        gs[i] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? deps[((long long)n * H + hh) * W + ww] : 0.f;
+    }
+    const int C4 = C >> 2, PP = 256 / C4;
+    const int c4 = (threadIdx.x % C4) * 4, pl = threadIdx.x / C4;
+    const bool active = pl < PP;
+    float wr[9][4];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wr[tap][j] = active ? w[(c4 + j) * 9 + tap] : 0.f;
+    __syncthreads();
+    float* dr = dz + ((long long)n * H + h) * W * lddz;
+    for (int x = active ? pl : W; x < W; x += PP) {
+        float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            // deps[h - (ky - 1)][x - (kx - 1)] = gs[ky][x + 2 - kx]
+            const float gv = gs[(tap / 3) * WP + x + 2 - tap % 3];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = fmaf(gv, wr[tap][j], o[j]);
+        }
+        st4(dr + (long long)x * lddz + c4, make_float4(o[0], o[1], o[2], o[3]));
     }
 }
 
@@ -855,11 +936,20 @@ CDM_API int cdm_philox_randint(int* out, int n, int lo, int hi, unsigned long lo
                        sub_dev);
     return cdm_status();
 }
+static int row_kernels() {   // $CDM_ROW_KERNELS: 1 (default) the row forms of the C_in = 1 / C_out = 1 kernels, 0 flat
+    static const int v = [] { const char* e = getenv("CDM_ROW_KERNELS"); return e ? atoi(e) : 1; }();
+    return v;
+}
 CDM_API int cdm_conv3x3_cin1_fwd(const float* x, int N, int H, int W, const float* w9, const float* bias, float* y,
                                  int ldy, int C, int relu, float* amax, void* stream) {
     if (C % 4) return (int)hipErrorInvalidValue;
     if (C > 1024) return (int)hipErrorInvalidValue;
     const long long P = (long long)N * H * W;
+    if (row_kernels() && W <= ROWK_MAXW && (long long)N * H <= 0x7fffffffll) {
+        hipLaunchKernelGGL(conv_cin1_fwd_row_kernel, dim3((unsigned)(N * H)), dim3(256), 3 * (W + 2) * sizeof(float),
+                           S(stream), x, H, W, w9, bias, y, ldy, C, relu, amax);
+        return cdm_status();
+    }
     hipLaunchKernelGGL(conv_cin1_fwd_kernel, dim3(nblocks(P, 256 / (C / 4), 4096)), dim3(256), 0, S(stream), x, N, H, W, w9,
                        bias, y, ldy, C, relu, amax);
     return cdm_status();
@@ -916,6 +1006,11 @@ CDM_API int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int 
                                     void* stream) {
     if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
     const long long P = (long long)N * H * W;
+    if (row_kernels() && W <= ROWK_MAXW && (long long)N * H <= 0x7fffffffll) {
+        hipLaunchKernelGGL(conv_cout1_dgrad_row_kernel, dim3((unsigned)(N * H)), dim3(256), 3 * (W + 2) * sizeof(float),
+                           S(stream), deps, H, W, C, w, dz, lddz);
+        return cdm_status();
+    }
     hipLaunchKernelGGL(conv_cout1_dgrad_kernel, dim3(nblocks(P, 256 / (C / 4), 4096)), dim3(256), 0, S(stream), deps, N, H,
                        W, C, w, dz, lddz);
     return cdm_status();

@@ -1,6 +1,7 @@
 """Child process of tests/test_gpu_kernels.py::test_deep_staging_bit_exact: runs the bf16 forward halo conv, whose
-staging schedule an environment switch selects ($CDM_HALO_DEEP, read once per process by the library), and the fused
-weight gradients on fixed seeded inputs and saves their outputs, so the test can compare two processes bit for bit.
+staging schedule an environment switch selects ($CDM_HALO_DEEP, read once per process by the library), the fused
+weight gradients, and the C_in = 1 forward / C_out = 1 input gradient (row or flat-pixel kernels: $CDM_ROW_KERNELS) on
+fixed seeded inputs and saves their outputs, so the test can compare two processes bit for bit.
 
     python tests/_variant_worker.py OUT.pt
 """
@@ -54,6 +55,20 @@ def main(out_path):
                                               None, None, None, am.data_ptr(), am.data_ptr() + 4, sp, slab.data_ptr(),
                                               nterm, s) == 0
             out[f"wgrad_{nterm}_{S}"] = slab.cpu()
+    # C_in = 1 forward and C_out = 1 input gradient: the row kernels vs the flat-pixel kernels ($CDM_ROW_KERNELS)
+    for (N, H, W, C) in ((3, 64, 64, 128), (2, 32, 32, 256), (2, 24, 40, 64), (1, 256, 256, 128)):
+        x1 = torch.randn(N * H * W, device="cuda", generator=g)
+        w9 = torch.randn(9 * C, device="cuda", generator=g) * 0.3
+        b1 = torch.randn(C, device="cuda", generator=g)
+        for relu in (0, 1):
+            y1 = torch.empty(N * H * W, C, device="cuda")
+            am = torch.zeros(1, device="cuda")
+            assert L.cdm_conv3x3_cin1_fwd(x1.data_ptr(), N, H, W, w9.data_ptr(), b1.data_ptr(), y1.data_ptr(), C, C,
+                                          relu, am.data_ptr(), s) == 0
+            out[f"cin1_{N}_{H}_{W}_{C}_{relu}"], out[f"cin1_amax_{N}_{H}_{W}_{C}_{relu}"] = y1.cpu(), am.cpu()
+        dz = torch.empty(N * H * W, C + 4, device="cuda")   # ld > C
+        assert L.cdm_conv3x3_cout1_dgrad(x1.data_ptr(), N, H, W, C, w9.data_ptr(), dz.data_ptr(), C + 4, s) == 0
+        out[f"cout1_dgrad_{N}_{H}_{W}_{C}"] = dz[:, :C].cpu()
     torch.cuda.synchronize()
     torch.save(out, out_path)
 

@@ -453,15 +453,16 @@ def test_bf16_halo_conv_vs_fp64(L, N, H, Cin, pre):
 
 def test_deep_staging_bit_exact(L, tmp_path):
     """The two-deep staging schedule of the bf16 forward halo conv (the halo two chunks ahead, $CDM_HALO_DEEP) produces
-    the one-ahead schedule's output bit for bit, and the fused weight gradients are reproducible across processes: the
-    same kernels in two child processes (tests/_variant_worker.py), the library reading the switch once per process."""
+    the one-ahead schedule's output bit for bit, the row forms of the C_in = 1 forward and C_out = 1 input gradient equal
+    the flat-pixel kernels bit for bit ($CDM_ROW_KERNELS), and the fused weight gradients are reproducible across
+    processes: two child processes (tests/_variant_worker.py), the library reading the switches once per process."""
     import subprocess
     import sys
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_variant_worker.py")
     outs = []
     for deep in ("1", "0"):
         f = tmp_path / f"deep{deep}.pt"
-        env = dict(os.environ, CDM_HALO_DEEP=deep)
+        env = dict(os.environ, CDM_HALO_DEEP=deep, CDM_ROW_KERNELS=deep)
         r = subprocess.run([sys.executable, worker, str(f)], env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(torch.load(f))
