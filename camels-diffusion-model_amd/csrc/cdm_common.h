@@ -61,7 +61,12 @@ static __device__ __forceinline__ void block_amax_commit(float m, float* out) {
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int i = 1; i < (int)((blockDim.x + 63) >> 6); ++i) m = fmaxf(m, red[i]);
-        atomicMax(reinterpret_cast<unsigned*>(out), __float_as_uint(m));
+        // *out only grows, so a block whose max does not exceed a value read from it has nothing to add: the atomic
+        // is skipped (a stale read only costs an unneeded atomic).  With one atomic per block on one address, the
+        // C_in = 1 forward's 16 384 blocks took 198 us against 94 us for the same kernel with no max requested.
+        const unsigned cur = __hip_atomic_load(reinterpret_cast<unsigned*>(out), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+        if (__float_as_uint(m) > cur) atomicMax(reinterpret_cast<unsigned*>(out), __float_as_uint(m));
     }
 }
 

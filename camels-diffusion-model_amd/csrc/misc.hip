@@ -157,20 +157,27 @@ __global__ __launch_bounds__(256) void conv_cin1_fwd_row_kernel(const float* __r
                                                                 int ldy, int C, int relu, float* amax) {
     extern __shared__ float xs[];   // [3][W + 2]
     const int n = blockIdx.x / H, h = blockIdx.x - n * H, WP = W + 2;
-    for (int i = threadIdx.x; i < 3 * WP; i += 256) {
-        const int r = i / WP, col = i - r * WP, hh = h + r - 1, ww = col - 1;
-        xs[i] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? x[((long long)n * H + hh) * W + ww] : 0.f;
-    }
     const int C4 = C >> 2, PP = 256 / C4;
     const int c4 = (threadIdx.x % C4) * 4, pl = threadIdx.x / C4;
     const bool active = pl < PP;
+    // weights and the source rows requested together (one memory round trip before the barrier, not two)
+    const int cw = active ? c4 : 0;
     float wr[9][4], bb[4];
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) wr[tap][j] = active ? w9[tap * C + c4 + j] : 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bb[j] = active ? bias[c4 + j] : 0.f;
+    for (int tap = 0; tap < 9; ++tap) {
+        const float4 v = ld4(w9 + tap * C + cw);
+        wr[tap][0] = v.x; wr[tap][1] = v.y; wr[tap][2] = v.z; wr[tap][3] = v.w;
+    }
+    {
+        const float4 v = ld4(bias + cw);
+        bb[0] = v.x; bb[1] = v.y; bb[2] = v.z; bb[3] = v.w;
+    }
+    for (int i = threadIdx.x; i < 3 * WP; i += 256) {
+        const int r = i / WP, col = i - r * WP, hh = h + r - 1, ww = col - 1;
+        const bool in = (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+        const float v = x[in ? ((long long)n * H + hh) * W + ww : 0];
+        xs[i] = in ? v : 0.f;
+    }
     __syncthreads();
     float am = 0.f;
     float* yr = y + ((long long)n * H + h) * W * ldy;
@@ -459,18 +466,22 @@ __global__ __launch_bounds__(256) void conv_cout1_dgrad_row_kernel(const float* 
                                                                    int lddz) {
     extern __shared__ float gs[];   // [3][W + 2]: gs[r][col] = deps[h + 1 - r][col - 1]
     const int n = blockIdx.x / H, h = blockIdx.x - n * H, WP = W + 2;
-    for (int i = threadIdx.x; i < 3 * WP; i += 256) {
-        const int r = i / WP, col = i - r * WP, hh = h + 1 - r, ww = col - 1;
-        gs[i] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? deps[((long long)n * H + hh) * W + ww] : 0.f;
-    }
     const int C4 = C >> 2, PP = 256 / C4;
     const int c4 = (threadIdx.x % C4) * 4, pl = threadIdx.x / C4;
     const bool active = pl < PP;
+    // weights and the source rows requested together (one memory round trip before the barrier, not two)
+    const int cw = active ? c4 : 0;
     float wr[9][4];
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wr[tap][j] = active ? w[(c4 + j) * 9 + tap] : 0.f;
+        for (int j = 0; j < 4; ++j) wr[tap][j] = w[(cw + j) * 9 + tap];
+    for (int i = threadIdx.x; i < 3 * WP; i += 256) {
+        const int r = i / WP, col = i - r * WP, hh = h + 1 - r, ww = col - 1;
+        const bool in = (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+        const float v = deps[in ? ((long long)n * H + hh) * W + ww : 0];
+        gs[i] = in ? v : 0.f;
+    }
     __syncthreads();
     float* dr = dz + ((long long)n * H + h) * W * lddz;
     for (int x = active ? pl : W; x < W; x += PP) {
