@@ -576,14 +576,24 @@ __global__ __launch_bounds__(256) void stats_mm_kernel(const float* __restrict__
         const int p0 = chunk * csize, p1 = min(HW, p0 + csize);
         Acc4<2> a;
         a.v[0] = f4zero(); a.v[1] = f4zero();
-        if (pl < P)
-            for (int p = p0 + pl; p < p1; p += P) {   // one read of y per element: StatsF's sums + max / min
-                const float4 v = ld4(y + ((long long)n * HW + p) * ldy + c4 * 4);
-                a.v[0].x += v.x; a.v[0].y += v.y; a.v[0].z += v.z; a.v[0].w += v.w;
-                a.v[1].x += v.x * v.x; a.v[1].y += v.y * v.y; a.v[1].z += v.z * v.z; a.v[1].w += v.w * v.w;
-                hi = make_float4(fmaxf(hi.x, v.x), fmaxf(hi.y, v.y), fmaxf(hi.z, v.z), fmaxf(hi.w, v.w));
-                lo = make_float4(fminf(lo.x, v.x), fminf(lo.y, v.y), fminf(lo.z, v.z), fminf(lo.w, v.w));
+        auto take = [&](const float4 v) {   // one read of y per element: StatsF's sums + max / min
+            a.v[0].x += v.x; a.v[0].y += v.y; a.v[0].z += v.z; a.v[0].w += v.w;
+            a.v[1].x += v.x * v.x; a.v[1].y += v.y * v.y; a.v[1].z += v.z * v.z; a.v[1].w += v.w * v.w;
+            hi = make_float4(fmaxf(hi.x, v.x), fmaxf(hi.y, v.y), fmaxf(hi.z, v.z), fmaxf(hi.w, v.w));
+            lo = make_float4(fminf(lo.x, v.x), fminf(lo.y, v.y), fminf(lo.z, v.z), fminf(lo.w, v.w));
+        };
+        if (pl < P) {
+            const float* yb = y + (long long)n * HW * ldy + c4 * 4;
+            int p = p0 + pl;
+            for (; p + 7 * P < p1; p += 8 * P) {   // 8 loads in flight, taken in the serial order (same sums)
+                float4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = ld4(yb + (long long)(p + u * P) * ldy);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) take(v[u]);
             }
+            for (; p < p1; p += P) take(ld4(yb + (long long)p * ldy));
+        }
         __syncthreads();   // red is reused per chunk
         if (pl < P) {
 #pragma unroll

@@ -35,6 +35,11 @@ f1 = t(lambda: L.cdm_conv3x3_cin1_fwd(x.data_ptr(), N, H, H, w9.data_ptr(), b.da
                                       am.data_ptr(), s))
 f0 = t(lambda: L.cdm_conv3x3_cin1_fwd(x.data_ptr(), N, H, H, w9.data_ptr(), b.data_ptr(), y.data_ptr(), C, C, 1, None, s))
 d = t(lambda: L.cdm_conv3x3_cout1_dgrad(x.data_ptr(), N, H, H, C, w9.data_ptr(), y.data_ptr(), C, s))
+from cdm_amd.engine import CHUNK  # noqa: E402
+nch = -(-H * H // CHUNK)
+slab = torch.empty(N * nch * 2 * C, device="cuda")
+ymm = torch.zeros(2 * C, dtype=torch.int32, device="cuda")
+sm = t(lambda: L.cdm_reduce_stats_mm(y.data_ptr(), C, N, H * H, C, CHUNK, slab.data_ptr(), ymm.data_ptr(), C, s))
 nb = P * C * 4
 print(f"CDM_ROW_KERNELS={os.environ.get('CDM_ROW_KERNELS', '1')}: cin1_fwd (amax) {f1:.1f} us {nb / f1 / 1e6:.2f} TB/s, "
-      f"cin1_fwd {f0:.1f} us, cout1_dgrad {d:.1f} us {nb / d / 1e6:.2f} TB/s")
+      f"cin1_fwd {f0:.1f} us, cout1_dgrad {d:.1f} us {nb / d / 1e6:.2f} TB/s, stats_mm {sm:.1f} us {nb / sm / 1e6:.2f} TB/s")
