@@ -164,17 +164,27 @@ HALO_FETCH_PER_BYTE = 0.6706
 
 
 def pmc_traffic(math: str):
-    """HBM bytes per launch of the dominant kernel from the committed PMC passes (tools/gpu_profile.sh):
-    FETCH_SIZE / 0.6706 (the halo staging pattern's calibrated counter rate) + WRITE_SIZE (exact for its stores), or
-    None when no profile has been collected."""
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes (tools/gpu_profile.sh), or None.
+
+    The 0.6706 FETCH_SIZE calibration holds for the LDS-halo conv's staging pattern only: it is applied to profiles of
+    a halo-kernel arithmetic (h3 / x6 / bf16) that carry FETCH_SIZE and WRITE_SIZE (KiB).  A profile with a plain
+    ``traffic_bytes`` (the round-1 fp32 gemm_f32_kernel pass) is reported as recorded; anything else gives None, so a
+    profile file of another shape never aborts the bench after its timed legs."""
     import glob
     suffix = "" if math == "fp32" else "_" + math
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_conv128{suffix}.json")))
     if not files:
         return None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return int((d["FETCH_SIZE"] / HALO_FETCH_PER_BYTE + d["WRITE_SIZE"]) * 1024)
+    try:
+        with open(files[-1]) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if math != "fp32" and "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+        return int((d["FETCH_SIZE"] / HALO_FETCH_PER_BYTE + d["WRITE_SIZE"]) * 1024)
+    if "traffic_bytes" in d:
+        return int(d["traffic_bytes"])
+    return None
 
 
 def _cpu_train_rate(R, nf: int, T: int, bs: int, steps: int, warmup: int):

@@ -91,15 +91,20 @@ class _BlockFunction(torch.autograd.Function):
     def forward(ctx, tape, out, n_in, *rest):
         ctx.tape, ctx.n_in = tape, n_in
         ctx.in_shapes = [tuple(x.shape) for x in rest[:n_in]]
-        ctx.params = rest[n_in:]
+        ctx.in_devices = [x.device for x in rest[:n_in]]
+        # the tape reads the live parameter storage at backward time (BatchNorm weights, biases, EmbedFC weights):
+        # saved here so that autograd's version check raises when one was modified in place in between
+        ctx.save_for_backward(*rest[n_in:])
         return out.view_as(out)
 
     @staticmethod
     def backward(ctx, gout):
+        params = ctx.saved_tensors          # raises if a parameter was updated in place after the forward
         tape = ctx.tape
         need = list(ctx.needs_input_grad[3:3 + ctx.n_in])
         gin = tape.backward(gout.detach().to(torch.float32).contiguous(), need, ctx.in_shapes)
-        pgrads = tuple(tape.grads.get(id(p)) for p in ctx.params)
+        gin = [None if g is None else g.to(d) for g, d in zip(gin, ctx.in_devices)]   # e.g. a CPU EmbedFC input
+        pgrads = tuple(tape.grads.get(id(p)) for p in params)
         return (None, None, None) + tuple(gin) + pgrads
 
 

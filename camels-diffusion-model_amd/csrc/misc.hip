@@ -316,6 +316,69 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_kernel(const float* z, int
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// image gradient of the init conv (ResidualConvBlock(1, nf, is_res) under autograd, diffusion_utilities.py:45-55):
+//   dx[p] = sum_{tap,c} W1[c][8 - tap] dy1[p + tap][c]  (conv1's input gradient: the tap-flipped 3x3 conv, C_out = 1)
+//         + sum_c scw[sel][c] gres[p][c]               (the random 1x1 shortcut's input gradient; sel = n >= split)
+// dy1 = bn_bwd_elem(g1, y1, ...) of conv1's BatchNorm + ReLU, applied while reading (bn.y == nullptr: g1 is dy1).
+// Same thread layout as conv_cout1_fwd_kernel: lanes over channels (float4), per-pixel sums folded through LDS.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv_cin1_dgrad_kernel(const float* g1, int ldg, Cin1BnBwd bn, const float* w9,
+                                                              const float* gres, int ldr, const float* scw, int split,
+                                                              int N, int H, int W, int C, float* dx) {
+    __shared__ float part[256];
+    const int C4 = C >> 2, PP = 256 / C4;
+    const int c4 = (threadIdx.x % C4) * 4, pl = threadIdx.x / C4;
+    float wr[9][4], cf[7][4];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wr[tap][j] = (pl < PP) ? w9[(c4 + j) * 9 + (8 - tap)] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cf[k][j] = (bn.y && pl < PP) ? bn.p[k][c4 + j] : 0.f;
+    const long long P = (long long)N * H * W;
+    for (long long base = (long long)blockIdx.x * PP; base < P; base += (long long)gridDim.x * PP) {
+        const long long pix = base + pl;
+        float s = 0.f;
+        if (pl < PP && pix < P) {
+            const int n = (int)(pix / (H * W)), rem = (int)(pix - (long long)n * H * W), h = rem / W, wx = rem - h * W;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int hh = h + tap / 3 - 1, ww = wx + tap % 3 - 1;
+                if ((unsigned)hh >= (unsigned)H || (unsigned)ww >= (unsigned)W) continue;
+                const long long q = ((long long)n * H + hh) * W + ww;
+                float4 v = ld4(g1 + q * ldg + c4);
+                if (bn.y) {
+                    const float4 yv = ld4(bn.y + q * bn.ldy + c4);
+                    float gv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        gv[j] = bn_bwd_elem(gv[j], f4get(yv, j), cf[0][j], cf[1][j], cf[2][j], cf[3][j], cf[4][j],
+                                            cf[5][j], cf[6][j]);
+                    v = make_float4(gv[0], gv[1], gv[2], gv[3]);
+                }
+                s = fmaf(v.x, wr[tap][0], s); s = fmaf(v.y, wr[tap][1], s);
+                s = fmaf(v.z, wr[tap][2], s); s = fmaf(v.w, wr[tap][3], s);
+            }
+            if (gres) {
+                const float* sw = scw + (n >= split ? C : 0) + c4;
+                const float4 r = ld4(gres + pix * ldr + c4);
+                s = fmaf(r.x, sw[0], s); s = fmaf(r.y, sw[1], s); s = fmaf(r.z, sw[2], s); s = fmaf(r.w, sw[3], s);
+            }
+        }
+        part[threadIdx.x] = s;
+        __syncthreads();
+        if (threadIdx.x < PP && base + threadIdx.x < P) {
+            float acc = 0.f;
+            for (int q = 0; q < C4; ++q) acc += part[threadIdx.x * C4 + q];
+            dx[base + threadIdx.x] = acc;
+        }
+        __syncthreads();
+    }
+}
+
 // Band form (W | 256, C % 16 == 0): a block owns R = 256/W whole output rows of one image.  The R + 2 input
 // rows of the band are staged through LDS 16 channels at a time (coalesced 64-byte pixel pieces); each thread
 // reduces its halo pixels to the 9 per-tap partial sums s[tap][q] = sum_c z[q][c] w[c][tap] (the weights are
@@ -697,6 +760,21 @@ __global__ __launch_bounds__(256) void embed_bwd_param_kernel(Mlp4 P) {
     }
 }
 
+// input gradient of two EmbedFCs fed the same input (timeembed1/2 by t, contextembed1/2 by c; ContextUnet.py:51-54):
+// dx[b][k] = sum_i dpre_a[b][i] w1_a[i][k] + sum_i dpre_b[b][i] w1_b[i][k]   (one thread per (b, k), sequential fp32)
+__global__ __launch_bounds__(256) void embed_input_grad_kernel(const float* dpre_a, const float* w1_a, int Ea,
+                                                               const float* dpre_b, const float* w1_b, int Eb, int rows,
+                                                               int in_dim, float* dx) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= rows * in_dim) return;
+    const int b = idx / in_dim, k = idx - b * in_dim;
+    float s = 0.f;
+    for (int i = 0; i < Ea; ++i) s = fmaf(dpre_a[(long long)b * Ea + i], w1_a[i * in_dim + k], s);
+    float s2 = 0.f;
+    for (int i = 0; i < Eb; ++i) s2 = fmaf(dpre_b[(long long)b * Eb + i], w1_b[i * in_dim + k], s2);
+    dx[idx] = s + s2;
+}
+
 // ------------------------------------------------------------------------------------------------
 // diffusion elementwise math
 // ------------------------------------------------------------------------------------------------
@@ -1013,6 +1091,18 @@ CDM_API int cdm_conv3x3_cout1_fwd_gn(const float* y, int ldy, int N, int H, int 
                        bias, out, gs, gt);
     return cdm_status();
 }
+CDM_API int cdm_conv3x3_cin1_dgrad(const float* g1, int ldg, const float* y1, int ldy, const float* s, const float* t,
+                                   const float* mean, const float* invstd, const float* A, const float* B,
+                                   const float* Cc, const float* w9, const float* gres, int ldr, const float* scw,
+                                   int split, int N, int H, int W, int C, float* dx, void* stream) {
+    if (C % 4 || C > 1024 || ldg % 4 || (y1 && ldy % 4) || (gres && (ldr % 4 || !scw))) return (int)hipErrorInvalidValue;
+    if (y1 && !(s && t && mean && invstd && A && B && Cc)) return (int)hipErrorInvalidValue;
+    const Cin1BnBwd bn{y1, ldy, {s, t, mean, invstd, A, B, Cc}};
+    const long long P = (long long)N * H * W;
+    hipLaunchKernelGGL(conv_cin1_dgrad_kernel, dim3(nblocks(P, 256 / (C / 4), 8192)), dim3(256), 0, S(stream), g1, ldg,
+                       bn, w9, gres, ldr, scw, split, N, H, W, C, dx);
+    return cdm_status();
+}
 CDM_API int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int C, const float* w, float* dz, int lddz,
                                     void* stream) {
     if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
@@ -1057,6 +1147,14 @@ CDM_API int cdm_embed_fwd(const Mlp4* P, void* stream) {
     int rows = 1;
     for (int k = 0; k < 4; ++k) { rows = P->m[k].rows > rows ? P->m[k].rows : rows; if (P->m[k].E > 1024) return (int)hipErrorInvalidValue; }
     hipLaunchKernelGGL(embed_fwd_kernel, dim3(rows, 4), dim3(256), 0, S(stream), *P);
+    return cdm_status();
+}
+CDM_API int cdm_embed_input_grad(const float* dpre_a, const float* w1_a, int Ea, const float* dpre_b,
+                                 const float* w1_b, int Eb, int rows, int in_dim, float* dx, void* stream) {
+    if (rows < 0 || in_dim < 1 || Ea < 0 || Eb < 0) return (int)hipErrorInvalidValue;
+    if (rows == 0) return 0;
+    hipLaunchKernelGGL(embed_input_grad_kernel, dim3((rows * in_dim + 255) / 256), dim3(256), 0, S(stream), dpre_a, w1_a,
+                       Ea, dpre_b, w1_b, Eb, rows, in_dim, dx);
     return cdm_status();
 }
 CDM_API int cdm_embed_bwd(const Mlp4* P, void* stream) {

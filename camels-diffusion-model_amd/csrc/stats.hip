@@ -1,4 +1,4 @@
-// Sample statistics of generated maps: 2-D power spectrum P(k) and per-map PDF.
+// Sample statistics of generated maps: power spectrum P(k) of 2-D / 3-D boxes and per-map PDF.
 //
 // Reference: power_spectrum  code/diffusion_utilities.py:302-368 (np.fft.fftn norm="ortho", bins round(k/dk))
 //            calculate_power_spectrum_2d  code/sample_power_spectra.py:112-165 (np.fft.fft2, log bins)
@@ -62,6 +62,49 @@ __global__ void dft_cols_power_kernel(const double2* __restrict__ T, int N, doub
         }
         power[((long long)b * N + u) * N + v] = (re * re + im * im) * scale;
     }
+}
+
+// Any-rank boxes (power_spectrum's 3-D branch and non-square 2-D boxes, diffusion_utilities.py:316-336): the DFT
+// along one axis of a complex fp64 array viewed as [outer][n][inner], one thread per output element (o, k, i):
+// out[o][k][i] = sum_j in[o][j][i] w^(k j).  Successive calls over every axis give fftn.  The input of the first pass is
+// the real fp32 box (re only); the last pass may write |F|^2 * scale instead of F.
+template <bool REAL_IN, bool POWER_OUT>
+__global__ __launch_bounds__(256) void dft_axis_kernel(const void* __restrict__ in_, int outer, int n, long long inner,
+                                                       double scale, void* __restrict__ out_) {
+    extern __shared__ double tw[];            // [2n]: cos, sin of 2 pi k / n
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        double s, c;
+        sincospi(2.0 * k / n, &s, &c);
+        tw[k] = c; tw[n + k] = s;
+    }
+    __syncthreads();
+    const long long total = (long long)outer * n * inner;
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const long long i = e % inner;
+    const long long ok = e / inner;
+    const int k = (int)(ok % n);
+    const long long o = ok / n;
+    const long long base = o * n * inner + i;
+    double re = 0.0, im = 0.0;
+    int idx = 0;
+    for (int j = 0; j < n; ++j) {             // w^(k j): angle index (k*j) mod n, accumulated
+        const double c = tw[idx], sn = tw[n + idx];
+        if constexpr (REAL_IN) {
+            const double v = (double)static_cast<const float*>(in_)[base + (long long)j * inner];
+            re = fma(v, c, re);
+            im = fma(-v, sn, im);
+        } else {                              // (a + i b)(c - i s)
+            const double2 v = static_cast<const double2*>(in_)[base + (long long)j * inner];
+            re = fma(v.x, c, fma(v.y, sn, re));
+            im = fma(v.y, c, fma(-v.x, sn, im));
+        }
+        idx += k; if (idx >= n) idx -= n;
+    }
+    if constexpr (POWER_OUT)
+        static_cast<double*>(out_)[e] = (re * re + im * im) * scale;
+    else
+        static_cast<double2*>(out_)[e] = make_double2(re, im);
 }
 
 // out[b][k] = sum over i in idx[off[k] .. off[k+1]) (in that order) of power[b][idx[i]]; one block per map
@@ -132,6 +175,47 @@ CDM_API int cdm_dft2_power(const float* img, int B, int N, double scale, void* T
     hipLaunchKernelGGL(dft_cols_power_kernel, dim3(B * N), dim3(th), 2 * N * sizeof(double), SS(stream),
                        reinterpret_cast<const double2*>(T), N, scale, power);
     return cdm_status();
+}
+
+// |fftn(box[b])|^2 * scale for B row-major boxes of rank 1..3 with extents dims[0..rank); T0 / T1 = scratch of
+// B * prod(dims) complex doubles each (ping-pong between the axis passes)
+CDM_API int cdm_dftn_power(const float* box, int B, int rank, const int* dims, double scale, void* T0, void* T1,
+                           double* power, void* stream) {
+    if (B < 0 || rank < 1 || rank > 3) return (int)hipErrorInvalidValue;
+    long long n_all = 1;
+    for (int a = 0; a < rank; ++a) {
+        if (dims[a] < 1 || dims[a] > 4096) return (int)hipErrorInvalidValue;
+        n_all *= dims[a];
+    }
+    if (B == 0) return 0;
+    const long long total = (long long)B * n_all;
+    const dim3 grid((unsigned)((total + 255) / 256));
+    long long inner = n_all;
+    const void* src = box;
+    void* bufs[2] = {T0, T1};
+    for (int a = 0; a < rank; ++a) {          // axis a: [B * prod(dims[:a])][dims[a]][prod(dims[a+1:])]
+        const int n = dims[a];
+        inner /= n;
+        const int outer = (int)(total / ((long long)n * inner));
+        const size_t sm = 2 * (size_t)n * sizeof(double);
+        const bool first = a == 0, last = a == rank - 1;
+        void* dst = last ? (void*)power : bufs[a & 1];
+        if (first && last)
+            hipLaunchKernelGGL((dft_axis_kernel<true, true>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
+                               scale, dst);
+        else if (first)
+            hipLaunchKernelGGL((dft_axis_kernel<true, false>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
+                               scale, dst);
+        else if (last)
+            hipLaunchKernelGGL((dft_axis_kernel<false, true>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
+                               scale, dst);
+        else
+            hipLaunchKernelGGL((dft_axis_kernel<false, false>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
+                               scale, dst);
+        int e = cdm_status(); if (e) return e;
+        src = dst;
+    }
+    return 0;
 }
 
 CDM_API int cdm_bin_sum(const double* power, int B, long long NN, const int* off, const int* idx, int nbins,

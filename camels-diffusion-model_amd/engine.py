@@ -142,7 +142,8 @@ class UNetEngine:
         self.kc_out0 = conv_kc(2 * n_feat, n_feat)
         self.pk: Dict[str, torch.Tensor] = {}
         self._pk_key = None
-        self._ones = torch.ones(4 * n_feat, device=self.device)
+        self.train_pack_token = None     # identity of the autograd forward whose train pack pk holds (model.py)
+        self._ones =torch.ones(4 * n_feat, device=self.device)
         self._zeros = torch.zeros(4 * n_feat, device=self.device)
         self._amax = torch.zeros(2, device=self.device)     # h3: max|A|, max|B| of the current launch
         # h3 train: batched repack (3 launches per step); $CDM_BATCH_REPACK=0 keeps the per-layer launches (A/B)
@@ -190,6 +191,7 @@ class UNetEngine:
     def repack(self, P: Dict[str, torch.Tensor], train: bool, stream: int, key=None):
         if key is not None and self._pk_key == (key, train):
             return
+        self.train_pack_token = None          # the pack changes owner (model.py re-packs before a stale backward)
         lb = lib(); nf = self.nf
         batched = train and self.nterm == NT_H3 and self.batch_repack
         if batched:
@@ -567,8 +569,13 @@ class UNetEngine:
     # backward (train mode workspaces only)
     # ------------------------------------------------------------------------------------------
     def backward(self, ws: "Workspace", P, deps: torch.Tensor, G: Dict[str, torch.Tensor], stream: int,
-                 out3_bias_done: bool = False, on_stage=None):
+                 out3_bias_done: bool = False, on_stage=None, dx: Optional[torch.Tensor] = None,
+                 dt: Optional[torch.Tensor] = None, dc: Optional[torch.Tensor] = None):
         """deps [B,H,W] = dL/d eps.  Writes (assigns) every parameter gradient into G[name].
+
+        Optional input gradients (the module API under autograd, ContextUnet.py:42-60): dx [B,H,W] = dL/dx (the
+        image), dt [rows_t] = dL/dt, dc [rows_c, n_cfeat] = dL/dc.  A t or c broadcast over the batch (one row) gets
+        its embedding gradients summed over the samples.
 
         ``on_stage(name)`` is called (on the host, in stream order) as soon as the gradients of a stage
         are final: "out", "up2", "up1", "up0emb", "down2", "down1", "init" — used to start the
@@ -657,10 +664,20 @@ class UNetEngine:
         d = ws._mlp
         for k, m in enumerate(MLPS):
             md = d.m[k]
-            md.dout = _p(ws.d_emb[m]); md.dpre = _p(ws.emb_dpre[m])
+            dout = ws.d_emb[m]
+            if md.rows == 1 and B > 1:          # t / c broadcast over the batch: one embedding row, sums over samples
+                E = dout.shape[1]
+                lb.cdm_col_sum(_p(dout), B, E, _p(ws.d_emb_row[m]), 0, s)
+                dout = ws.d_emb_row[m]
+            md.dout = _p(dout); md.dpre = _p(ws.emb_dpre[m])
             md.dw1 = _p(G[m + ".model.0.weight"]); md.db1 = _p(G[m + ".model.0.bias"])
             md.dw2 = _p(G[m + ".model.2.weight"]); md.db2 = _p(G[m + ".model.2.bias"])
         lb.cdm_embed_bwd(ctypes_addr(d), s)
+        for dv, (ma, mb), rows, in_dim in ((dt, ("timeembed1", "timeembed2"), ws.t_rows, 1),
+                                           (dc, ("contextembed1", "contextembed2"), ws.c_rows, self.ncf)):
+            if dv is not None:
+                lb.cdm_embed_input_grad(_p(ws.emb_dpre[ma]), _p(P[ma + ".model.0.weight"]), 2 * nf,
+                                        _p(ws.emb_dpre[mb]), _p(P[mb + ".model.0.weight"]), nf, rows, in_dim, _p(dv), s)
         hook("up0emb")
         # ---------------- down2, down1, init ----------------
         self._chain_bwd(ws, P, self.layers[6:10], G, s)
@@ -668,7 +685,29 @@ class UNetEngine:
         self._chain_bwd(ws, P, self.layers[2:6], G, s)
         hook("down1")
         self._chain_bwd(ws, P, self.layers[0:2], G, s)
+        if dx is not None:
+            self._image_grad(ws, P, dx, s)
         hook("init")
+
+    def _image_grad(self, ws, P, dx: torch.Tensor, s: int):
+        """dL/dx of the image (ResidualConvBlock(1, nf, is_res) at diffusion_utilities.py:45-55 under autograd):
+        init_conv.conv1's input gradient (the tap-flipped 3x3 conv over its BatchNorm + ReLU backward, applied while
+        reading g and y) plus the random 1x1 shortcut's (sum_c w[c] * grad of the block output).  Runs after the init
+        conv's backward, whose BatchNorm coefficients ws.coef still hold."""
+        l = self.layers[0]
+        C, B, H = l.cout, ws.B, self.H
+        st, co = ws.bn[l.name], ws.coef
+        g = ws.gout[l.name]
+        gres = ws.gout["init_conv.conv2"]
+        sc_w, _, split = ws.sc_pending
+        if self.fuse_cin1_bwd:
+            lib().cdm_conv3x3_cin1_dgrad(g.p, g.ld, _p(ws.y[l.name]), C, _p(st["scale"]), _p(st["shift"]),
+                                         _p(st["mean"]), _p(st["invstd"]), _p(co[0]), _p(co[1]), _p(co[2]),
+                                         _p(P[l.w]), gres.p, gres.ld, _p(sc_w), split, B, H, H, C, _p(dx), s)
+        else:                                   # dy1 was written by cdm_norm_apply_bwd
+            dy = ws.dy[l.name]
+            lib().cdm_conv3x3_cin1_dgrad(dy.p, dy.ld, None, 0, None, None, None, None, None, None, None, _p(P[l.w]),
+                                         gres.p, gres.ld, _p(sc_w), split, B, H, H, C, _p(dx), s)
 
     def _chain_bwd(self, ws, P, layers, G, s):
         for l in reversed(layers):
@@ -941,6 +980,7 @@ class Workspace:
             self.emb_h = {m: E(B, (2 if m.endswith("1") else 1) * nf) for m in MLPS}
             self.emb_dpre = {m: E(B, (2 if m.endswith("1") else 1) * nf) for m in MLPS}
             self.d_emb = {m: E(B, (2 if m.endswith("1") else 1) * nf) for m in MLPS}
+            self.d_emb_row = {m: E(1, (2 if m.endswith("1") else 1) * nf) for m in MLPS}   # broadcast t / c
         self.gn0 = {k: E(B * 2 * nf) for k in ("mean", "invstd", "scale", "shift")}
         self.gnO = {k: E(B * nf) for k in ("mean", "invstd", "scale", "shift")}
         # per conv-BN layer: y (pre-norm), z destinations, BN coefficients

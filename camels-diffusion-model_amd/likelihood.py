@@ -253,9 +253,12 @@ def _sched_tensors(timesteps, ab_t, b_t, a_t):
     b = torch.as_tensor(b_t).detach().to("cpu", torch.float32).reshape(-1)
     a = (1 - b) if a_t is None else torch.as_tensor(a_t).detach().to("cpu", torch.float32).reshape(-1)
     ab = torch.as_tensor(ab_t).detach().to("cpu", torch.float32).reshape(-1)
-    if not (b.numel() == a.numel() == ab.numel() == int(timesteps) + 1):
-        raise ValueError(f"schedule tensors must have timesteps + 1 = {int(timesteps) + 1} entries")
-    return b, a, ab
+    # the reference only indexes [t] for t <= timesteps, so a longer schedule (e.g. built for a larger T) works there
+    # too: its first timesteps + 1 entries are the ones read
+    n = int(timesteps) + 1
+    if min(b.numel(), a.numel(), ab.numel()) < n:
+        raise ValueError(f"schedule tensors need at least timesteps + 1 = {n} entries")
+    return b[:n].contiguous(), a[:n].contiguous(), ab[:n].contiguous()
 
 
 def _evaluator(model, timesteps, noise_source="device", sched=None) -> LikelihoodEvaluator:

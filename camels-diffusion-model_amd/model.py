@@ -139,22 +139,36 @@ class _UNetFunction(torch.autograd.Function):
         s = _stream()
         B = x.shape[0]
         eng.repack(P, True, s)
+        ctx.pack_token = eng.train_pack_token = object()   # whose weights the engine's train pack holds
         ws = eng.workspace(B, True)
         eps = eng.forward(ws, P, x.reshape(B, mod.h, mod.h), t, c, sc_w, sc_b, B, s)
         mod._invalidate_eval_pack()
         ctx.state = (mod, eng, ws, P)
+        # the engine backward reads the live parameters (BatchNorm weights, ConvT / EmbedFC weights): saved so that
+        # autograd's version check raises if one was updated in place between forward and backward
+        ctx.save_for_backward(*params)
         return eps.view(B, 1, mod.h, mod.h)
 
     @staticmethod
     def backward(ctx, geps):
+        ctx.saved_tensors                   # version check of the parameters
         mod, eng, ws, P = ctx.state
-        if ws.t_rows != ws.B or ws.c_rows != ws.B:
-            raise NotImplementedError("backward needs per-sample t and c (the reference training step's shapes)")
         names = mod._param_names
+        if getattr(eng, "train_pack_token", None) is not ctx.pack_token:
+            # another forward (another model of this shape, or an eval pack) re-used the engine's packed weights in
+            # between: re-pack this model's (unchanged, version-checked) parameters for its dgrads
+            eng.repack(P, True, _stream())
+            eng.train_pack_token = ctx.pack_token
         G = {n: torch.empty_like(P[n]) for n in names}
-        eng.backward(ws, P, geps.reshape(ws.B, mod.h, mod.h).contiguous(), G, _stream())
+        dev = geps.device
+        need_x, need_t, need_c = ctx.needs_input_grad[1:4]
+        dx = torch.empty(ws.B, mod.h, mod.h, device=dev) if need_x else None
+        dt = torch.empty(ws.t_rows, device=dev) if need_t else None
+        dc = torch.empty(ws.c_rows, mod.n_cfeat, device=dev) if need_c else None
+        eng.backward(ws, P, geps.reshape(ws.B, mod.h, mod.h).contiguous(), G, _stream(), dx=dx, dt=dt, dc=dc)
         ctx.state = None
-        return (None, None, None, None, None, None, *[G[n] for n in names])
+        return (None, None if dx is None else dx.view(ws.B, 1, mod.h, mod.h), dt, dc, None, None,
+                *[G[n] for n in names])
 
 
 class _EvalNoBackward(torch.autograd.Function):
@@ -255,7 +269,8 @@ class ContextUnet(nn.Module):
         if c is not None:
             c = c.to(device=dev, dtype=torch.float32).reshape(-1, self.n_cfeat).contiguous()
         sc_w, sc_b = self.draw_shortcut(dev)
-        needs_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        needs_grad = torch.is_grad_enabled() and (any(p.requires_grad for p in self.parameters())
+                                                  or any(v is not None and v.requires_grad for v in (x, t, c)))
         if self.training and needs_grad:
             return _UNetFunction.apply((self,), x, t, c, sc_w, sc_b, *[P[n] for n in self._param_names])
         s = _stream()

@@ -14,7 +14,8 @@ Batched device entry points: ``power_spectra(images, dl)`` ([B, N, N] -> [B, nbi
 Split of work: the per-map O(N^3) fp64 DFT + |F|^2, the per-bin power sums and the per-map histograms run
 in csrc/stats.hip; the bin geometry (which frequency goes to which bin, in the reference's summation
 order) depends only on N and dl and is built once on the host with the reference's own expressions.
-2-D maps only: the reference's 3-D branch of power_spectrum is not used by any of its scripts.
+power_spectrum also takes 3-D and non-square 2-D boxes (its reference branch at diffusion_utilities.py:316-336): one
+direct-DFT pass per axis (cdm_dftn_power) and the same host-built bin geometry.
 """
 from __future__ import annotations
 
@@ -33,17 +34,20 @@ def _s():
 
 
 @lru_cache(maxsize=16)
-def _radial_geometry(N: int, dl: float):
-    """power_spectrum's bins (diffusion_utilities.py:325-341): CSR lists of flat indices per bin, flat order."""
-    k1 = 2 * np.pi * np.fft.fftfreq(N, dl)
-    kx, ky = np.meshgrid(k1, k1, indexing="ij")
-    kgrid = np.sqrt(kx ** 2 + ky ** 2)
-    dk = 2 * np.pi / (N * dl)
+def _radial_geometry(dims, dl: float):
+    """power_spectrum's bins (diffusion_utilities.py:325-341) for a box of extents ``dims`` (2-D or 3-D): CSR lists of
+    flat indices per bin, flat order."""
+    if isinstance(dims, int):
+        dims = (dims, dims)
+    comps = [2 * np.pi * np.fft.fftfreq(d, dl) for d in dims]
+    grids = np.meshgrid(*comps, indexing="ij")
+    kgrid = np.sqrt(sum(g ** 2 for g in grids))      # kx**2 + ky**2 (+ kz**2), the reference's order of additions
+    dk = 2 * np.pi / (np.min(dims) * dl)
     n_bins = int(np.ceil(np.max(kgrid) / dk)) + 1
     kf = kgrid.flatten()
     bins = np.array([int(round(v / dk)) for v in kf])
     keep = bins < n_bins
-    order = np.arange(N * N)[keep]
+    order = np.arange(kf.size)[keep]
     b = bins[keep]
     srt = np.argsort(b, kind="stable")                 # stable: flat order inside each bin
     idx = order[srt].astype(np.int32)
@@ -94,36 +98,57 @@ def _power(x: torch.Tensor, scale: float) -> torch.Tensor:
 
 
 def _bin_sums(P: torch.Tensor, idx: np.ndarray, off: np.ndarray) -> torch.Tensor:
-    B, N = P.shape[0], P.shape[1]
+    B, NN = P.shape[0], P[0].numel()
     nb = len(off) - 1
     di = torch.from_numpy(idx).to(P.device)
     do = torch.from_numpy(off).to(P.device)
     out = torch.empty(B, nb, dtype=torch.float64, device=P.device)
-    lib().cdm_bin_sum(P.data_ptr(), B, N * N, do.data_ptr(), di.data_ptr(), nb, out.data_ptr(), _s())
+    lib().cdm_bin_sum(P.data_ptr(), B, NN, do.data_ptr(), di.data_ptr(), nb, out.data_ptr(), _s())
     torch.cuda.current_stream().synchronize()               # di / do are temporaries
     return out
 
 
-def power_spectra(images, dl: float = 1.0) -> Tuple[np.ndarray, torch.Tensor]:
-    """Batched power_spectrum: (k_bins [nbins], pk [B, nbins] fp64 on the device)."""
-    x = _as_maps(images)
-    N = x.shape[1]
-    k, idx, off, count = _radial_geometry(N, float(dl))
-    P = _power(x, 1.0 / (N * N))                            # |fftn(norm="ortho")|^2 = |F|^2 / N^2
+def _power_nd(x: torch.Tensor, dims, scale: float) -> torch.Tensor:
+    """|fftn|^2 * scale of B boxes x [B, *dims] (any rank <= 3, any extents): one DFT pass per axis."""
+    import ctypes
+    B = x.shape[0]
+    n = int(np.prod(dims))
+    T0 = torch.empty(B * n * 2, dtype=torch.float64, device=x.device)
+    T1 = torch.empty(B * n * 2, dtype=torch.float64, device=x.device) if len(dims) > 2 else T0
+    P = torch.empty(B, n, dtype=torch.float64, device=x.device)
+    d = (ctypes.c_int * len(dims))(*dims)          # read by the host entry point before it returns
+    lib().cdm_dftn_power(x.data_ptr(), B, len(dims), ctypes.addressof(d), float(scale), T0.data_ptr(), T1.data_ptr(),
+                         P.data_ptr(), _s())
+    return P
+
+
+def _binned(P: torch.Tensor, dims, dl: float):
+    k, idx, off, count = _radial_geometry(tuple(dims), float(dl))
     s = _bin_sums(P, idx, off)
     cnt = torch.from_numpy(count).to(s.device)
-    pk = torch.where(cnt > 0, s / cnt.clamp(min=1), s) * (dl ** 2)   # :359-363
-    return k, pk
+    return k, torch.where(cnt > 0, s / cnt.clamp(min=1), s) * (dl ** len(dims))   # :359-363
+
+
+def power_spectra(images, dl: float = 1.0) -> Tuple[np.ndarray, torch.Tensor]:
+    """Batched power_spectrum of square 2-D maps: (k_bins [nbins], pk [B, nbins] fp64 on the device)."""
+    x = _as_maps(images)
+    N = x.shape[1]
+    P = _power(x, 1.0 / (N * N))                            # |fftn(norm="ortho")|^2 = |F|^2 / N^2
+    return _binned(P, (N, N), dl)
 
 
 def power_spectrum(box, dl: float = 1.0):
-    """diffusion_utilities.py:302-368 for a 2-D box -> (k_bins, pk) numpy."""
+    """diffusion_utilities.py:302-368 for a 2-D or 3-D box (any extents) -> (k_bins, pk) numpy."""
     b = np.asarray(box.detach().cpu() if torch.is_tensor(box) else box)
-    if b.ndim == 3:
-        raise NotImplementedError("3-D boxes: the reference's scripts only use 2-D maps")
-    if b.ndim != 2:
+    if b.ndim not in (2, 3):
         raise ValueError("Input box must be 2D or 3D")
-    k, pk = power_spectra(b, dl)
+    if b.ndim == 2 and b.shape[0] == b.shape[1]:
+        k, pk = power_spectra(b, dl)
+        return k, pk[0].cpu().numpy()
+    dims = tuple(int(v) for v in b.shape)
+    x = torch.from_numpy(np.ascontiguousarray(b, np.float32)).to("cuda").reshape(1, -1)
+    P = _power_nd(x, dims, 1.0 / float(np.prod(dims)))      # norm="ortho": |F|^2 / prod(dims)
+    k, pk = _binned(P, dims, dl)
     return k, pk[0].cpu().numpy()
 
 

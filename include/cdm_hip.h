@@ -154,6 +154,11 @@ int cdm_amax_f32(const float* x, long long rows, int C, long long ld, float* out
  * B*N*N complex doubles).  scale 1/N^2 = np.fft.fftn(norm="ortho") of power_spectrum, diffusion_utilities.py:322;
  * scale 1 = np.fft.fft2 of calculate_power_spectrum_2d, sample_power_spectra.py:128. */
 int cdm_dft2_power(const float* img, int B, int N, double scale, void* T, double* power, void* stream);
+/* power[b] = |fftn(box[b])|^2 * scale, fp64, for B row-major boxes of rank 1..3 with extents dims[0..rank) (host
+ * array): one direct-DFT pass per axis; T0, T1 = scratch of B * prod(dims) complex doubles each.  The 3-D and non-square
+ * branches of power_spectrum (diffusion_utilities.py:316-336). */
+int cdm_dftn_power(const float* box, int B, int rank, const int* dims, double scale, void* T0, void* T1, double* power,
+                   void* stream);
 /* out[b][k] = sum_{i = off[k]}^{off[k+1]-1} power[b][idx[i]] in list order (the reference's binning loops,
  * diffusion_utilities.py:352-356 / sample_power_spectra.py:157-163, with the bin geometry built on the host) */
 int cdm_bin_sum(const double* power, int B, long long NN, const int* off, const int* idx, int nbins, double* out,
@@ -283,6 +288,14 @@ int cdm_conv3x3_cout1_fwd(const float* z, int ldz, int N, int H, int W, int C, c
  * C % 16 == 0, W | 256, (256 / W) | H. */
 int cdm_conv3x3_cout1_fwd_gn(const float* y, int ldy, int N, int H, int W, int C, const float* gs, const float* gt,
                              const float* w, const float* bias, float* out, void* stream);
+/* image gradient of the init conv (ResidualConvBlock(1, nf, is_res) under autograd, diffusion_utilities.py:45-55):
+ * dx[n][p] = sum_{tap,c} w9[c][8 - tap] dy1[p + tap][c] + sum_c scw[(n >= split) * C + c] gres[p][c], w9 = conv1's OIHW
+ * weights [C][1][3][3]; dy1 = the BatchNorm + ReLU backward of g1 with y1 and the coefficients of cdm_norm_apply_bwd
+ * mode 0 (y1 == NULL: g1 is dy1); gres = the gradient of the block output (NULL: no shortcut term). */
+int cdm_conv3x3_cin1_dgrad(const float* g1, int ldg, const float* y1, int ldy, const float* s, const float* t,
+                           const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
+                           const float* w9, const float* gres, int ldr, const float* scw, int split, int N, int H,
+                           int W, int C, float* dx, void* stream);
 int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int C, const float* w, float* dz, int lddz,
                             void* stream);
 /* weight gradient partials: csize > 0: per (image, csize-pixel chunk) [N][chunks][9][C]; csize = -R (band form, H % R
@@ -294,6 +307,10 @@ int cdm_avgpool_gelu_fin(const float* sums, int N, int C, int HW, float* hpre, f
 int cdm_avgpool_gelu_bwd(const float* dhv, const float* hpre, int N, int HW, int C, float* dst, int ldd, void* stream);
 /* EmbedFC x4 (diffusion_utilities.py:118-145); `P` points to a host struct cdm_mlp4 (see csrc/misc.hip MlpDesc) */
 int cdm_embed_fwd(const void* P, void* stream);
+/* input gradient of the two EmbedFCs fed one input (t: timeembed1/2, c: contextembed1/2; ContextUnet.py:51-54):
+ * dx[b][k] = sum_i dpre_a[b][i] w1_a[i][k] + sum_i dpre_b[b][i] w1_b[i][k]  (dpre from cdm_embed_bwd, w1 [E][in_dim]) */
+int cdm_embed_input_grad(const float* dpre_a, const float* w1_a, int Ea, const float* dpre_b, const float* w1_b, int Eb,
+                         int rows, int in_dim, float* dx, void* stream);
 int cdm_embed_bwd(const void* P, void* stream);
 /* perturb_input (code/train_diffusion_condition.py:202-203) + t/T for the time embedding (:225).
  * t: per-sample steps, or cur_i: one device-side step for the batch with noise row (T - *cur_i)*nstride. */

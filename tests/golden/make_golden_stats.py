@@ -101,6 +101,13 @@ def main():
     out["pdf_bin_mid"] = np.asarray(ax0[0][0])
     out["pdf_train_mean"], out["pdf_test_mean"] = np.asarray(ax0[0][1]), np.asarray(ax0[1][1])
     out["pdf_train_std"], out["pdf_test_std"] = np.asarray(ax1[0][1]), np.asarray(ax1[1][1])
+    # round 4: the 3-D branch and non-square boxes of power_spectrum (diffusion_utilities.py:316-363), from a
+    # generator of their own (the arrays above are unchanged)
+    r3 = np.random.default_rng(2025)
+    for tag, shape, dl in (("ps3_a", (16, 20, 24), 0.5), ("ps3_b", (24, 24, 24), 1.0), ("ps_ns", (24, 40), 1.0)):
+        box = r3.uniform(0, 1, size=shape).astype(np.float32)
+        k, pk = du.power_spectrum(box, dl)
+        out[tag + "_box"], out[tag + "_k"], out[tag + "_pk"], out[tag + "_dl"] = box, k, pk, np.float64(dl)
     np.savez_compressed(os.path.join(HERE, "stats.npz"), **out)
     print({k: np.shape(v) for k, v in out.items()})
 

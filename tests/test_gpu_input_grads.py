@@ -1,0 +1,144 @@
+"""Input gradients through ContextUnet under autograd (the reference is an ordinary nn.Module, ContextUnet.py:42-60):
+d loss / d x (the image), d loss / d t and d loss / d c, with per-sample and with broadcast t / c (one row, the shapes
+code/diffusion_utilities.py:137-145 views to [-1, in_dim]), against torch autograd of the CPU oracle.
+
+Tolerance: relative L2 of each input gradient (and, for the broadcast case, of every parameter gradient) vs an fp64
+autograd run of the oracle, at most 3x the reference's own fp32 deviation from that fp64 run plus a floor of 2e-6 (the
+fp32 rounding of a gradient the network barely amplifies).  Train-mode BatchNorm, n_feat = 16, B = 4.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu as R
+import _parity
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+NF, NCF, H, B = 16, 6, 64, 4
+
+
+def _rel_l2(a, b):
+    a = torch.as_tensor(a).double().cpu(); b = torch.as_tensor(b).double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
+
+
+def _oracle(sd, x, t, c, sc, dtype, weight):
+    """autograd of the oracle forward (train mode) -> (eps, dx, dt, dc, param grads)."""
+    sd = {k: (v.to(dtype) if v.is_floating_point() else v.clone()).clone() for k, v in sd.items()}
+    keys = [k for k, _, kind in R.state_dict_layout(1, NF, NCF, H) if kind == "param"]
+    for k in keys:
+        sd[k].requires_grad_(True)
+    xx = x.to(dtype).clone().requires_grad_(True)
+    tt = t.to(dtype).clone().requires_grad_(True)
+    cc = c.to(dtype).clone().requires_grad_(True)
+    eps = R.unet_forward(sd, xx, tt, cc, n_feat=NF, n_cfeat=NCF, height=H, train=True,
+                         shortcut=(sc[0].to(dtype), sc[1].to(dtype)))
+    (eps * weight.to(dtype)).sum().backward()
+    return eps.detach(), xx.grad, tt.grad, cc.grad, {k: sd[k].grad for k in keys}
+
+
+@pytest.mark.parametrize("math", ["fp32", "h3"])
+@pytest.mark.parametrize("bcast", [False, True])
+def test_input_grads_vs_autograd(math, bcast):
+    import cdm_amd
+    torch.manual_seed(3)
+    m = cdm_amd.ContextUnet(1, NF, NCF, H, conv_math=math).cuda().train()
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, 1, H, H, generator=g)
+    rows = 1 if bcast else B
+    t = torch.rand(rows, generator=g)
+    c = torch.rand(rows, NCF, generator=g)
+    weight = torch.randn(B, 1, H, H, generator=g)
+    torch.manual_seed(21)
+    sc = R.draw_shortcut(1, NF)                  # the draw the module makes below
+    xg, tg, cg = (v.cuda().requires_grad_(True) for v in (x, t, c))
+    torch.manual_seed(21)
+    eps = m(xg, tg, cg)
+    (eps * weight.cuda()).sum().backward()
+    e64, dx64, dt64, dc64, g64 = _oracle(sd, x, t, c, sc, torch.float64, weight)
+    e32, dx32, dt32, dc32, g32 = _oracle(sd, x, t, c, sc, torch.float32, weight)
+    assert _rel_l2(eps.detach(), e64) <= 3 * _rel_l2(e32, e64) + 2e-6
+    rec = {}
+    for name, hip, r64, r32 in (("x", xg.grad.view(B, 1, H, H), dx64, dx32), ("t", tg.grad, dt64, dt32),
+                                ("c", cg.grad, dc64, dc32)):
+        assert hip is not None and tuple(hip.shape) == tuple(r64.shape), name
+        eh, er = _rel_l2(hip, r64), _rel_l2(r32, r64)
+        rec[name] = (eh, er)
+        assert eh <= 3 * er + 2e-6, f"d/d{name}: HIP {eh:.3e} vs reference fp32 {er:.3e}"
+    worst = 0.0
+    if bcast:                                    # the embedding gradients summed over the batch
+        for k, p in m.named_parameters():
+            eh, er = _rel_l2(p.grad, g64[k]), _rel_l2(g32[k], g64[k])
+            worst = max(worst, eh / (3 * er + 2e-6))
+            assert eh <= 3 * er + 2e-6, f"{k}: HIP {eh:.3e} vs reference fp32 {er:.3e}"
+    _parity.record("input_grads", conv_math=math, broadcast=bcast,
+                   errors={k: {"hip": a, "ref32": b} for k, (a, b) in rec.items()}, worst_param_ratio=worst)
+
+
+def test_input_grad_only_x():
+    """x.requires_grad with frozen parameters: the image gradient alone (the use a caller of d eps / dx makes)."""
+    import cdm_amd
+    torch.manual_seed(4)
+    m = cdm_amd.ContextUnet(1, NF, NCF, H).cuda().train()
+    for p in m.parameters():
+        p.requires_grad_(False)
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(B, 1, H, H, generator=g)
+    t, c = torch.rand(B, generator=g), torch.rand(B, NCF, generator=g)
+    weight = torch.randn(B, 1, H, H, generator=g)
+    torch.manual_seed(22)
+    sc = R.draw_shortcut(1, NF)
+    xg = x.cuda().requires_grad_(True)
+    torch.manual_seed(22)
+    eps = m(xg, t.cuda(), c.cuda())
+    (eps * weight.cuda()).sum().backward()
+    _, dx64, _, _, _ = _oracle(sd, x, t, c, sc, torch.float64, weight)
+    _, dx32, _, _, _ = _oracle(sd, x, t, c, sc, torch.float32, weight)
+    assert _rel_l2(xg.grad, dx64) <= 3 * _rel_l2(dx32, dx64) + 2e-6
+    assert all(p.grad is None for p in m.parameters())
+
+
+def test_inplace_update_between_forward_and_backward_raises():
+    """A parameter modified in place after the forward: autograd's version check raises."""
+    import cdm_amd
+    torch.manual_seed(5)
+    m = cdm_amd.ContextUnet(1, 8, NCF, H).cuda().train()
+    x = torch.randn(2, 1, H, H, device="cuda")
+    eps = m(x, torch.rand(2, device="cuda"), torch.rand(2, NCF, device="cuda"))
+    with torch.no_grad():
+        m.up0[1].weight.add_(1.0)
+    with pytest.raises(RuntimeError):
+        eps.sum().backward()
+
+
+def test_two_models_interleaved_backward():
+    """Forward model A, forward model B (same shape: one shared engine and weight pack), then backward A: A's gradients
+    are computed with A's weights (the pack is rebuilt for A), equal to A's forward + backward run alone."""
+    import cdm_amd
+    x = torch.randn(2, 1, H, H, generator=torch.Generator().manual_seed(1)).cuda()
+    t, c = torch.rand(2).cuda(), torch.rand(2, NCF).cuda()
+    grads = []
+    for interleave in (False, True):
+        torch.manual_seed(6)
+        a = cdm_amd.ContextUnet(1, 8, NCF, H).cuda().train()
+        torch.manual_seed(7)
+        b = cdm_amd.ContextUnet(1, 8, NCF, H).cuda().train()
+        torch.manual_seed(30)
+        ea = a(x, t, c)
+        if interleave:
+            torch.manual_seed(31)
+            b(x, t, c)
+        ea.sum().backward()
+        grads.append({k: p.grad.clone() for k, p in a.named_parameters()})
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k

@@ -51,6 +51,18 @@ def test_power_spectrum_matches_reference(fx, tag, box):
     _close(pk, S.power_spectrum(img.astype(np.float64), dl)[1])
 
 
+@pytest.mark.parametrize("tag", ["ps3_a", "ps3_b", "ps_ns"])
+def test_power_spectrum_3d_and_non_square(fx, tag):
+    """3-D boxes (16x20x24 at dl=0.5, 24^3) and a 24x40 map: the per-axis DFT path (cdm_dftn_power) vs the
+    reference's own values and the fp64 oracle."""
+    import cdm_amd
+    box, dl = fx[tag + "_box"], float(fx[tag + "_dl"])
+    k, pk = cdm_amd.power_spectrum(box, dl)
+    np.testing.assert_array_equal(k, fx[tag + "_k"])
+    _close(pk, fx[tag + "_pk"], **F32REF)
+    _close(pk, S.power_spectrum(box.astype(np.float64), dl)[1])
+
+
 def test_compare_power_spectra_matches_reference(fx, tmp_path):
     import cdm_amd
     k, om, gm = cdm_amd.compare_power_spectra(torch.from_numpy(fx["orig"][:, None]),

@@ -52,3 +52,11 @@ def test_compare_distributions(fx):
     _close(trs, fx["pdf_train_std"])
     _close(tem, fx["pdf_test_mean"])
     _close(tes, fx["pdf_test_std"])
+
+
+@pytest.mark.parametrize("tag", ["ps3_a", "ps3_b", "ps_ns"])
+def test_power_spectrum_3d_and_non_square(fx, tag):
+    """The 3-D branch and a non-square 2-D box of power_spectrum (diffusion_utilities.py:316-363)."""
+    k, pk = S.power_spectrum(fx[tag + "_box"], float(fx[tag + "_dl"]))
+    _close(k, fx[tag + "_k"])
+    _close(pk, fx[tag + "_pk"])
