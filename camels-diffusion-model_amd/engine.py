@@ -151,6 +151,9 @@ class UNetEngine:
         # measurement hook: probe(args) before every 3x3 conv launch, args = the _conv3x3 arguments (bench.py replays
         # the dominant conv's launches of a real train step on their real operands); None in production
         self.launch_probe = None
+        # diagnostic hook: stage_probe(stage, ws) at fixed points of the forward ("x0", "d1", "d2", "emb", "film2", "u3";
+        # tools/t1500_steps.py substitutes reference values there to locate an error source); None in production
+        self.stage_probe = None
         self._batch_key = None
 
     # ------------------------------------------------------------------------------------------
@@ -410,8 +413,11 @@ class UNetEngine:
             lb.cdm_fill_i32(_p(ws.ymm), half, -2 ** 31, s)               # max keys
             lb.cdm_fill_i32(_p(ws.ymm) + 4 * half, half, 2 ** 31 - 1, s)  # min keys
         # ---------------- encoder ----------------
-        for l in self.layers[:10]:
+        probe = self.stage_probe or (lambda stage, ws_: None)
+        for i, l in enumerate(self.layers[:10]):
             self._conv_bn_fwd(ws, P, l, s, x)
+            if i in (1, 5, 9):
+                probe({1: "x0", 5: "d1", 9: "d2"}[i], ws)
         # ---------------- to_vec ----------------
         d2 = ws.catU1.sl(2 * nf, 2 * nf)
         lb.cdm_reduce_sum(d2.p, d2.ld, B, H2 * H2, 2 * nf, H2 * H2, _p(ws.hsum), s)
@@ -437,6 +443,7 @@ class UNetEngine:
             md.out = _p(ws.emb[m])
         lb.cdm_embed_fwd(ctypes_addr(d), s)
         ws._mlp = d
+        probe("emb", ws)
         # ---------------- up0: ConvT(k=h/4) on the 1x1 map, GroupNorm(8), ReLU, FiLM1 -> catU1[:, :2nf] ----
         c0 = 2 * nf
         if self.up0_large:
@@ -454,10 +461,12 @@ class UNetEngine:
         self.convT2x2(ws, "up1.model.0", ws.catU1, B, H2, 4 * nf, P, ws.yT1, "catU1", "yT1", s)
         for l in self.layers[10:14]:
             self._conv_bn_fwd(ws, P, l, s, x)
+        probe("film2", ws)
         # ---------------- up2 ----------------
         self.convT2x2(ws, "up2.model.0", ws.catU2, B, H1, 2 * nf, P, ws.yT2, "catU2", "yT2", s)
         for l in self.layers[14:18]:
             self._conv_bn_fwd(ws, P, l, s, x)
+        probe("u3", ws)
         # ---------------- out ----------------
         self.conv3x3("out.0.wpk", ws.catO.p, B, H, 2 * nf, 2 * nf, _p(P["out.0.bias"]), _p(ws.yO), nf, nf, 0,
                      _p(ws.slab), nf, self.kc_out0, s, amax_x=self._slot(ws, "catO"))

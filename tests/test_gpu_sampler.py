@@ -155,6 +155,41 @@ def test_sample_T1500_matches_reference(w, math):
         assert e <= 3 * er + floor, f"snapshot {s}: {e:.3e} vs reference {er:.3e}"
 
 
+@pytest.mark.parametrize("w", [0.0, 3.0])
+def test_sample_nf128_matches_reference(w):
+    """The benchmarked width: sample_ddpm (code/train_diffusion_condition.py:281-335) at n_feat = 128 (seeded default
+    init, the reference's own weights for torch.manual_seed(0)), n = 2, w = 0 and the batched 2n CFG forward at w = 3,
+    T = 400, CPU-RNG replay, vs the reference's trajectory re-run in fp64 (tests/golden/make_golden_r4.py).  Every layer
+    runs the bench's kernels: the LDS-halo eval convs with BatchNorm folded, out.1's GroupNorm in out.3's staging, the
+    16-bit ConvT.  Bar: final x and every stored snapshot within 3x the reference's own fp32 deviation from fp64 at that
+    snapshot, plus one fp32 rounding of max|x| (2^-23)."""
+    import cdm_amd
+    sfx = np.load(os.path.join(GOLD, "sampler_T400_nf128.npz"))
+    T, nf = int(sfx["T"]), int(sfx["n_feat"])
+    torch.manual_seed(int(sfx["init_seed"]))
+    m = cdm_amd.ContextUnet(1, nf, 6, 64).cuda().eval()
+    d = cdm_amd.DDPM(m, T, "cuda", z_source="host")
+    torch.manual_seed(int(sfx[f"w{w:g}_seed"]))
+    x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(sfx["params"]), w)
+    x = x.cpu().numpy()
+    ref64, ref32 = sfx[f"w{w:g}_x_fp64"], sfx[f"w{w:g}_x"]
+    mx = np.abs(ref64).max()
+    e_hip, e_ref = np.abs(x - ref64).max() / mx, np.abs(ref32 - ref64).max() / mx
+    floor = 2.0 ** -23
+    snaps = []
+    for j, sl in enumerate(sfx["snap_keep"]):
+        r = sfx[f"w{w:g}_inter_fp64"][j]
+        rm = np.abs(r).max()
+        snaps.append((int(sl), float(np.abs(inter[sl] - r).max() / rm), float(np.abs(sfx[f"w{w:g}_inter"][j] - r).max() / rm)))
+    print(f"nf=128 T={T} w={w:g} [{m.conv_math}]: vs fp64 HIP {e_hip:.2e}, reference fp32 {e_ref:.2e}; snapshots "
+          + " ".join(f"{a}:{b:.1e}/{c:.1e}" for a, b, c in snaps))
+    _parity.record("sample_nf128_T400", w=w, conv_math=m.conv_math, max_abs_x=float(mx), final_err=float(e_hip),
+                   final_err_ref32=float(e_ref), snapshots=[{"slot": a, "err": b, "err_ref32": c} for a, b, c in snaps])
+    assert e_hip <= 3 * e_ref + floor, (e_hip, e_ref)
+    for sl, e, er in snaps:
+        assert e <= 3 * er + floor, f"snapshot {sl}: {e:.3e} vs reference {er:.3e}"
+
+
 def test_device_z_fresh_per_call_and_seedable():
     """z_source="device": consecutive sampling calls draw fresh z (the reference's randn_like on the device), and
     torch.manual_seed makes a call reproducible (the captured graph used to replay one z sequence)."""

@@ -105,7 +105,8 @@ def main():
               f" {'ratio':>6s}")
         for k in ("x0", "d1", "d2", "hv", "cemb1", "temb1", "cemb2", "temb2", "y0", "film1", "film2", "u3", "yO",
                   "eps"):
-            r = I64[k].double(); h_ = hip[k].reshape(r.shape); c_ = I32[k].double().reshape(r.shape)
+            r = I64[k].double(); c_ = I32[k].double().reshape(r.shape)
+            h_ = hip[k].reshape(-1)[: r.numel()].reshape(r.shape)   # broadcast t: one embedding row written
             mx = r.abs().max().item()
             l2 = r.norm().item()
             eh, ec = (h_ - r).abs().max().item() / mx, (c_ - r).abs().max().item() / mx
