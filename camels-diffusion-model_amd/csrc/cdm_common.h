@@ -16,6 +16,33 @@ static __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f,
 static __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 static __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
+// ---- activation element types (C4 mixed precision stores the fused Conv -> BN -> ReLU chain's y and g as bf16) ----
+// Act<T>::Raw is what a 4-channel piece occupies in registers between its load and its use (loads stay raw so the
+// conversion does not force a wait at the load site); to4() widens it (bf16 -> fp32 is exact); round() is the value a
+// store of v keeps.
+template <class T> struct Act;
+template <> struct Act<float> {
+    typedef float4 Raw;
+    static __device__ __forceinline__ Raw load4(const void* p) { return *reinterpret_cast<const float4*>(p); }
+    static __device__ __forceinline__ float4 to4(const Raw& r) { return r; }
+    static __device__ __forceinline__ Raw zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+    static __device__ __forceinline__ float round(float v) { return v; }
+    static __device__ __forceinline__ void store(float* p, float v) { *p = v; }
+    static __device__ __forceinline__ float load(const float* p) { return *p; }
+};
+template <> struct Act<__bf16> {
+    typedef uint2 Raw;
+    static __device__ __forceinline__ Raw load4(const void* p) { return *reinterpret_cast<const uint2*>(p); }
+    static __device__ __forceinline__ float4 to4(const Raw& r) {
+        return make_float4(__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u), __uint_as_float(r.y << 16),
+                           __uint_as_float(r.y & 0xffff0000u));
+    }
+    static __device__ __forceinline__ Raw zero() { return make_uint2(0u, 0u); }
+    static __device__ __forceinline__ float round(float v) { return (float)(__bf16)v; }
+    static __device__ __forceinline__ void store(__bf16* p, float v) { *p = (__bf16)v; }
+    static __device__ __forceinline__ float load(const __bf16* p) { return (float)*p; }
+};
+
 static __device__ __forceinline__ float f4get(const float4& v, int j) {
     return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
 }
@@ -30,6 +57,8 @@ static __device__ __forceinline__ float fkey_inv(int k) { return __int_as_float(
 
 // exact (erf) GELU, as torch.nn.GELU() default (diffusion_utilities.py:130, ContextUnet.py:17)
 static __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// GELU evaluated in fp64 (rounded once by the caller): the per-step embeddings / to_vec (csrc/misc.hip)
+static __device__ __forceinline__ double gelu_d(double x) { return 0.5 * x * (1.0 + erf(x * 0.70710678118654752440)); }
 static __device__ __forceinline__ float gelu_grad_f(float x) {
     const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
     const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);

@@ -175,9 +175,11 @@ struct LdConvT2x2GatherB {  // convT 2x2 wgrad: B(k = input pix (n,h,w), n = ij*
 
 enum { EPI_RELU = 1, EPI_ACCUM = 2 };
 
-template <int WM = 2>   // WM = waves along M (2: 128-row block, 4: 256-row block); stats per 128-row tile
+// WM = waves along M (2: 128-row block, 4: 256-row block); stats per 128-row tile.  OT = the stored element type (bf16:
+// C4's fused-chain activations and gradients; the statistics / maxima are those of the stored, rounded values)
+template <int WM = 2, class OT = float>
 struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-tile column stats
-    float* y; long long ldy; long long zstride; const float* bias; int bias_mod; int flags;
+    OT* y; long long ldy; long long zstride; const float* bias; int bias_mod; int flags;
     float* stats; int stats_ld;  // stats[tile][0|1][stats_ld]: sum / sum of squares of the stored value
     int M, N;
     float* amax = nullptr;       // optional running max|stored value| (block_amax_commit)
@@ -185,7 +187,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
     int ymm_ld = 0;              //   ymm[n] (atomic max), ymm[ymm_ld + n] (atomic min); needs stats
     __device__ __forceinline__ void operator()(f32x16 (&acc)[2][2], int mw, int nw, int lane, int wm, int wn,
                                                float* scratch, int tid) const {
-        float* yz = y + (long long)blockIdx.z * zstride;   // 0 when the kernel applied its own (remapped) slab
+        OT* yz = y + (long long)blockIdx.z * zstride;      // 0 when the kernel applied its own (remapped) slab
         float cs[2] = {0.f, 0.f}, cq[2] = {0.f, 0.f};
         float cmx[2] = {-INFINITY, -INFINITY}, cmn[2] = {INFINITY, INFINITY};
         float am = 0.f;
@@ -199,9 +201,10 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
             const bool accum = flags & EPI_ACCUM;
             CDM_FOR_ACC({
                 float v = acc[i][j][r] + bj[j];
-                if (accum) v += yz[(long long)m * ldy + n];
+                if (accum) v += Act<OT>::load(yz + (long long)m * ldy + n);
                 if (relu) v = relu_f(v);
-                yz[(long long)m * ldy + n] = v;
+                v = Act<OT>::round(v);
+                Act<OT>::store(yz + (long long)m * ldy + n, v);
                 cs[j] += v; cq[j] += v * v;
                 am = fmaxf(am, fabsf(v));
                 cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
@@ -211,10 +214,11 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
                 if (m < M && n < N) {
                     float v = acc[i][j][r];
                     if (bias) v += bias[n % bias_mod];
-                    float* p = yz + (long long)m * ldy + n;
-                    if (flags & EPI_ACCUM) v += *p;
+                    OT* p = yz + (long long)m * ldy + n;
+                    if (flags & EPI_ACCUM) v += Act<OT>::load(p);
                     if (flags & EPI_RELU) v = relu_f(v);
-                    *p = v;
+                    v = Act<OT>::round(v);
+                    Act<OT>::store(p, v);
                     cs[j] += v; cq[j] += v * v;
                     am = fmaxf(am, fabsf(v));
                     cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
@@ -278,7 +282,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
 };
 using EpiStore = EpiStoreW<2>;
 template <class EP> struct IsEpiStoreW : std::false_type {};
-template <int WM> struct IsEpiStoreW<EpiStoreW<WM>> : std::true_type {};
+template <int WM, class OT> struct IsEpiStoreW<EpiStoreW<WM, OT>> : std::true_type {};
 
 struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n, 2h+i, 2w+j, co] = acc + b[co]
     float* y; long long ldy; const float* bias; int H, W, Co, M, N;
@@ -892,8 +896,9 @@ constexpr int HTHREADS = 512;
 // tap's first MFMA, 256 staggered halo split (waves 0-3 split + store the next chunk's halo after their last kernel
 // row's MFMAs, waves 4-7 before them, so each SIMD pairs one wave's VALU with its partner's MFMAs), 512 static
 // priority 1 for waves 4-7
-template <int NT, int WT, class EP, bool XCD_REMAP, int ABL = (NT >= 6 ? 0 : 1), class PRE = PreNone>
-__global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const float* __restrict__ x, int H, int Cin,
+// XT: element type of the source x (and of PRE's y): bf16 for C4's fused-chain activations / gradients
+template <int NT, int WT, class EP, bool XCD_REMAP, int ABL = (NT >= 6 ? 0 : 1), class PRE = PreNone, class XT = float>
+__global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* __restrict__ x, int H, int Cin,
                                                                       int ldx, const __bf16* __restrict__ wx3,
                                                                       int Cout, const float* amax_x,
                                                                       const float* amax_w, EP ep, PRE pre,
@@ -963,14 +968,16 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     // address and are zeroed where they are stored): with loads under branches the compiler can no longer count
     // them and waits for vmcnt(0) — the B stores of a kernel row then waited on the next chunk's halo (HBM latency)
     // and the halo split on the B loads just issued.
-    float4 hreg[HQ];
+    using RawX = typename Act<XT>::Raw;
+    constexpr unsigned XSZ = sizeof(XT);
+    RawX hreg[HQ];
     // chunk-0 source of piece j as a 32-bit byte offset from the uniform base x (pre.y): scalar base + lane offset
     // loads, one VGPR per piece instead of a 64-bit pointer (the PreBnBwd variant spilled with two pointers per piece).
     // Offsets stay below 2^32: the host checks N H W ldx * 4 bytes < 2^32 (cdm_conv3x3 entry points).
     unsigned hxo[HQ];               // (a dummy in-bounds offset 0 + channel quad when !hin[j])
     bool hin[HQ];                   // piece j is inside the image (else zero padding / past the halo)
     int hdst[HQ];                   // its LDS offset within a term plane
-    float4 yreg[PRE::on ? HQ : 1];  // PreBnBwd: the pre-norm activations of piece j
+    RawX yreg[PRE::on ? HQ : 1];    // PreBnBwd: the pre-norm activations of piece j
     unsigned hyo[PRE::on ? HQ : 1];
     auto setup_tile = [&](int t) {  // halo source offsets of tile t
         const int m0 = t * HBM_, img = m0 / hw, h0 = (m0 - img * hw) / WT;
@@ -983,8 +990,8 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
             const bool in = q < HPX * 4 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)WT;
             const unsigned pix = in ? (unsigned)((img * H + ih) * WT + iw) : 0u;
             hin[j] = in;
-            hxo[j] = (pix * (unsigned)ldx + (unsigned)c4 * 4u) * 4u;
-            if constexpr (PRE::on) hyo[j] = (pix * (unsigned)pre.ldy + (unsigned)c4 * 4u) * 4u;
+            hxo[j] = (pix * (unsigned)ldx + (unsigned)c4 * 4u) * XSZ;
+            if constexpr (PRE::on) hyo[j] = (pix * (unsigned)pre.ldy + (unsigned)c4 * 4u) * XSZ;
         }
     };
 #pragma unroll
@@ -994,12 +1001,12 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     }
     setup_tile(t_first);
     // a halo register set and its in-image mask (DEEP: the mask travels with the set across a tile change)
-    auto gload_halo_to = [&](float4 (&dst)[HQ], unsigned& mask, int cc) {
+    auto gload_halo_to = [&](RawX (&dst)[HQ], unsigned& mask, int cc) {
         const char* xb = reinterpret_cast<const char*>(x + cc * 16);
         mask = 0u;
 #pragma unroll
         for (int j = 0; j < HQ; ++j) {
-            dst[j] = *reinterpret_cast<const float4*>(xb + hxo[j]);
+            dst[j] = Act<XT>::load4(xb + hxo[j]);
             mask |= (hin[j] ? 1u : 0u) << j;
         }
     };
@@ -1009,15 +1016,15 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         }
         const char* xb = reinterpret_cast<const char*>(x + cc * 16);
 #pragma unroll
-        for (int j = 0; j < HQ; ++j) hreg[j] = *reinterpret_cast<const float4*>(xb + hxo[j]);
+        for (int j = 0; j < HQ; ++j) hreg[j] = Act<XT>::load4(xb + hxo[j]);
         if constexpr (PRE::on) {
-            const char* yb = reinterpret_cast<const char*>(pre.y + cc * 16);
+            const char* yb = reinterpret_cast<const char*>(pre.y) + (size_t)cc * 16 * XSZ;   // pre.y holds XT elements
 #pragma unroll
-            for (int j = 0; j < HQ; ++j) yreg[j] = *reinterpret_cast<const float4*>(yb + hyo[j]);
+            for (int j = 0; j < HQ; ++j) yreg[j] = Act<XT>::load4(yb + hyo[j]);
         }
     };
     // inb(j): piece j lies inside the image (else zero padding)
-    auto store_halo_impl = [&](const float4 (&src)[HQ], auto inb, __bf16* base, int cc) {
+    auto store_halo_impl = [&](const RawX (&src)[HQ], auto inb, __bf16* base, int cc) {
         float cf[NCOEF ? NCOEF : 1][4];   // coefficients of this thread's 4 channels (q & 3 == tid & 3 for every j)
         if constexpr (NCOEF > 0) {
             const int cb = cc * 16 + (tid & 3) * 4;
@@ -1030,11 +1037,13 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
 #pragma unroll
         for (int j = 0; j < HQ; ++j) {
             if (HPAD || hdst[j] >= 0) {
-                float xv[4] = {src[j].x, src[j].y, src[j].z, src[j].w};
+                const float4 sv = Act<XT>::to4(src[j]);
+                float xv[4] = {sv.x, sv.y, sv.z, sv.w};
                 if constexpr (PRE::kind == 1) {
+                    const float4 yv = Act<XT>::to4(yreg[j]);
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
-                        xv[e] = bn_bwd_elem(xv[e], f4get(yreg[j], e), cf[0][e], cf[1][e], cf[2][e], cf[3][e],
+                        xv[e] = bn_bwd_elem(xv[e], f4get(yv, e), cf[0][e], cf[1][e], cf[2][e], cf[3][e],
                                             cf[4][e], cf[5][e], cf[6][e]);
                 } else if constexpr (PRE::kind == 2) {
 #pragma unroll
@@ -1061,7 +1070,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
         }
     };
     auto store_halo = [&](__bf16* base, int cc) { store_halo_impl(hreg, [&](int j) { return hin[j]; }, base, cc); };
-    auto store_halo_set = [&](const float4 (&src)[HQ], unsigned mask, __bf16* base, int cc) {
+    auto store_halo_set = [&](const RawX (&src)[HQ], unsigned mask, __bf16* base, int cc) {
         store_halo_impl(src, [&](int j) { return ((mask >> j) & 1u) != 0u; }, base, cc);
     };
     // ---- B staging: piece q = (plane q>>8 = dx*NS + t, col (q&255)>>1, k-half q&1) of group g ----
@@ -1246,7 +1255,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     int hb = 0, bb = 0;
     // DEEP: set X holds the chunk after the current one (stored at the end of the current chunk), set Y receives the
     // one after that; the roles alternate per chunk (nchunks is even, so they line up across tiles)
-    float4 hX[DEEP ? HQ : 1], hY[DEEP ? HQ : 1];
+    RawX hX[DEEP ? HQ : 1], hY[DEEP ? HQ : 1];
     unsigned mX = 0u, mY = 0u;
     if constexpr (DEEP) gload_halo_to(hX, mX, 1);
     for (int kt = 0, t = t_first; kt < tpb && t < mtiles; ++kt, t += t_step) {
@@ -1260,7 +1269,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const floa
     if constexpr (DEEP) {
     // chunk cc: B of chunk q+1 and the halo of chunk q+2 are loaded (across the tile end: the next tile's chunks 0 / 1),
     // the MFMAs of chunk q run, then chunk q+1 (halo from the set loaded one chunk earlier) is stored
-    auto step = [&](int cc, const float4 (&hs)[HQ], unsigned ms, float4 (&hl)[HQ], unsigned& ml) {
+    auto step = [&](int cc, const RawX (&hs)[HQ], unsigned ms, RawX (&hl)[HQ], unsigned& ml) {
         const bool morec = cc + 1 < nchunks;
         const bool has1 = morec || nextt;               // chunk q+1 exists in this block
         const __bf16* a = Hs + hb * NS * HPLANE;
@@ -1527,13 +1536,15 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
 // kx shift), so each dY fragment feeds 3 taps and X is staged once instead of three times (2.5x less LDS
 // traffic per MFMA than the per-tap kernel above).  8 waves = 2 (co) x 4 (ci), wave tile 64 co x 32 ci x 3
 // taps (6 accumulators).  Split-K over pixel ranges; writes slab[z][co][tap*Cin+ci] like the per-tap kernel.
-template <int NT, int KS = 1, class PRE = PreNone, class PX = PreNone>
+template <int NT, int KS = 1, class PRE = PreNone, class PX = PreNone, class GT = float, class XT = float>
+                                // GT / XT: element types of dy (g and PRE's y) / of x (and PX's g): bf16 for C4's
+                                // fused-chain activations and gradients
                                 // KS: 16-pixel K steps per barrier (W % (16 KS) == 0);
                                 // KS = 2: 1.09x KS = 1 (KS = 4 needs 133 KB of LDS: the launch is refused)
                                 // PRE = PreBnBwd: dy computed from g (the dy argument) and y while staging
                                 // PX = PreBnRelu: X = relu(y s + t) computed from the previous layer's y (the x argument)
-__global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __restrict__ dy, int lddy, int Cout,
-                                                              const float* __restrict__ x, int H, int W, int Cin,
+__global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restrict__ dy, int lddy, int Cout,
+                                                              const XT* __restrict__ x, int H, int W, int Cin,
                                                               int ldx, int ktiles, int kt_per_split,
                                                               const float* amax_dy, const float* amax_x,
                                                               float* __restrict__ slab, PRE pre, PX px, int stg) {
@@ -1571,7 +1582,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
     const int hw = H * W;
     const int p0 = kt0 * RA;
     int pn = p0 / hw, ph = (p0 - pn * hw) / W, pw = p0 - pn * hw - ph * W;
-    float4 ra[KS], rb[KS], rb1 = f4zero();
+    using RawG = typename Act<GT>::Raw;
+    using RawX = typename Act<XT>::Raw;
+    RawG ra[KS];
+    RawX rb[KS], rb1 = Act<XT>::zero();
     bool vb[KS], vb1 = false;       // PX: which X pieces lie inside the image (padding stays zero)
     float xs[4], xt[4];             // PX coefficients of this thread's 4 input channels ci0 + c4
     if constexpr (PX::kind >= 2) {
@@ -1585,14 +1599,14 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
     constexpr bool SUMS = PX::kind == 3;
     bool sum_step = false;
     float xm[4], xi[4], s1[4], s2[4], s5[4];
-    float4 gr[SUMS ? KS : 1], gr1 = f4zero();
+    RawX gr[SUMS ? KS : 1], gr1 = Act<XT>::zero();
     if constexpr (SUMS) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) { s1[e] = 0.f; s2[e] = 0.f; s5[e] = 0.f; }
         const float4 a = ld4(px.mean + ci0 + c4), b = ld4(px.invstd + ci0 + c4);
         xm[0] = a.x; xm[1] = a.y; xm[2] = a.z; xm[3] = a.w; xi[0] = b.x; xi[1] = b.y; xi[2] = b.z; xi[3] = b.w;
     }
-    float4 ya[PRE::on ? KS : 1];
+    RawG ya[PRE::on ? KS : 1];
     float cf[PRE::on ? 7 : 1][4];   // PreBnBwd coefficients of this thread's 4 output channels m0 + c4
     if constexpr (PRE::on) {
 #pragma unroll
@@ -1613,20 +1627,25 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
             const long long pix = (long long)(pn * H + ph) * W + pw + sr + 16 * k;
-            ra[k] = ld4(dy + pix * lddy + m0 + c4);
-            if constexpr (PRE::on) ya[k] = ld4(pre.y + pix * pre.ldy + m0 + c4);
+            ra[k] = Act<GT>::load4(dy + pix * lddy + m0 + c4);
+            if constexpr (PRE::on) ya[k] = Act<GT>::load4(reinterpret_cast<const GT*>(pre.y) + pix * pre.ldy + m0 + c4);
             const int w0 = pw - 1 + sr + 16 * k;
             vb[k] = rowok && (unsigned)w0 < (unsigned)W;
-            rb[k] = vb[k] ? ld4(x + (xrow + w0) * ldx + ci0 + c4) : f4zero();
+            rb[k] = vb[k] ? Act<XT>::load4(x + (xrow + w0) * ldx + ci0 + c4) : Act<XT>::zero();
             if constexpr (SUMS) {   // central rows 1..RA of the X image (the step's own columns, inside the image)
-                gr[k] = (sum_step && (k > 0 || sr >= 1)) ? ld4(px.g + (xrow + w0) * px.ldg + ci0 + c4) : f4zero();
+                gr[k] = (sum_step && (k > 0 || sr >= 1))
+                            ? Act<XT>::load4(reinterpret_cast<const XT*>(px.g) + (xrow + w0) * px.ldg + ci0 + c4)
+                            : Act<XT>::zero();
             }
         }
         if (tid < 64) {
             const int w1 = pw + RA - 1 + sr;
             vb1 = rowok && w1 < W;
-            rb1 = vb1 ? ld4(x + (xrow + w1) * ldx + ci0 + c4) : f4zero();
-            if constexpr (SUMS) gr1 = (sum_step && tid < 32) ? ld4(px.g + (xrow + w1) * px.ldg + ci0 + c4) : f4zero();
+            rb1 = vb1 ? Act<XT>::load4(x + (xrow + w1) * ldx + ci0 + c4) : Act<XT>::zero();
+            if constexpr (SUMS)
+                gr1 = (sum_step && tid < 32)
+                          ? Act<XT>::load4(reinterpret_cast<const XT*>(px.g) + (xrow + w1) * px.ldg + ci0 + c4)
+                          : Act<XT>::zero();
         }
         pw += RA;
         if (pw >= W) { pw = 0; if (++ph == H) { ph = 0; ++pn; } }
@@ -1666,25 +1685,28 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const float* __res
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
             if constexpr (PRE::on) {
-                const float yv[4] = {ya[k].x, ya[k].y, ya[k].z, ya[k].w};
-                float gv[4] = {ra[k].x, ra[k].y, ra[k].z, ra[k].w};
+                const float4 yf = Act<GT>::to4(ya[k]), gf = Act<GT>::to4(ra[k]);
+                const float yv[4] = {yf.x, yf.y, yf.z, yf.w};
+                float gv[4] = {gf.x, gf.y, gf.z, gf.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     gv[e] = bn_bwd_elem(gv[e], yv[e], cf[0][e], cf[1][e], cf[2][e], cf[3][e], cf[4][e], cf[5][e],
                                         cf[6][e]);
                 put(a, sr + 16 * k, make_float4(gv[0], gv[1], gv[2], gv[3]), sa, IA);
             } else {
-                put(a, sr + 16 * k, ra[k], sa, IA);
+                put(a, sr + 16 * k, Act<GT>::to4(ra[k]), sa, IA);
             }
+            const float4 xk = Act<XT>::to4(rb[k]);
             if constexpr (SUMS) {
-                if (sum_step && (k > 0 || sr >= 1)) xsum(rb[k], gr[k]);
+                if (sum_step && (k > 0 || sr >= 1)) xsum(xk, Act<XT>::to4(gr[k]));
             }
-            put(b, sr + 16 * k, xpre(rb[k], vb[k]), sb, IB);
+            put(b, sr + 16 * k, xpre(xk, vb[k]), sb, IB);
         }
+        const float4 x1 = Act<XT>::to4(rb1);
         if constexpr (SUMS) {
-            if (sum_step && tid < 32) xsum(rb1, gr1);
+            if (sum_step && tid < 32) xsum(x1, Act<XT>::to4(gr1));
         }
-        if (tid < 64) put(b, RA + sr, xpre(rb1, vb1), sb, IB);
+        if (tid < 64) put(b, RA + sr, xpre(x1, vb1), sb, IB);
     };
     // transposed-read addresses (see the per-tap kernel); tap t reads X rows shifted by t
     const int g = (lane >> 4) & 3, q = (lane >> 2) & 3, pq = lane & 3;
@@ -1843,31 +1865,40 @@ static int halo_deep() {
     return v;
 }
 
-template <int WT, class PRE = PreNone>
-static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
-                            const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm, hipStream_t s,
+// XT / OT: element types of the source (x, PRE's y) and of the stored output; bf16 only with the one-term (C4)
+// arithmetic
+template <int WT, class PRE = PreNone, class XT = float, class OT = float>
+static int launch_conv_halo(const XT* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
+                            const float* amax_x, const float* amax_w, const EpiStoreW<4, OT>& ep, int nterm, hipStream_t s,
                             PRE pre = PRE{}, int tpb = 0) {
+    using EP = EpiStoreW<4, OT>;
+    constexpr bool F32 = std::is_same<XT, float>::value && std::is_same<OT, float>::value;
     const int M = N * H * WT, mtiles = M / HBM_;
     // the kernel addresses the halo sources (x, pre.y) by 32-bit byte offsets from their base
-    if ((unsigned long long)M * (unsigned)ldx * 4ull >= (1ull << 32)) return (int)hipErrorInvalidValue;
+    if ((unsigned long long)M * (unsigned)ldx * sizeof(XT) >= (1ull << 32)) return (int)hipErrorInvalidValue;
     if constexpr (PRE::kind == 1) {
-        if ((unsigned long long)M * (unsigned)pre.ldy * 4ull >= (1ull << 32)) return (int)hipErrorInvalidValue;
+        if ((unsigned long long)M * (unsigned)pre.ldy * sizeof(XT) >= (1ull << 32)) return (int)hipErrorInvalidValue;
     }
+    if (!F32 && nterm != 1) return (int)hipErrorInvalidValue;
     if (tpb < 1) tpb = halo_tpb(mtiles, (Cout + GBN - 1) / GBN, nterm, WT);
     dim3 grid((mtiles + tpb - 1) / tpb, (Cout + GBN - 1) / GBN, 1);
     if constexpr (WT > 64) {
         // wide rows (C5: 128 / 256 columns): a block is 256 / WT whole rows, halo (256/WT + 2) x (WT + 2);
         // LDS fits the two-term (h3) image only (WT 256: 2 x 2 x 774 px x 32 B + 48 KiB B = 145 KiB)
-        if (nterm != NT_H3) return (int)hipErrorInvalidValue;
-        hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EpiStoreW<4>, true, 1, PRE>), grid, dim3(HTHREADS), 0, s,
-                           x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm));
-        return cdm_status();
+        if constexpr (!F32) {
+            return (int)hipErrorInvalidValue;
+        } else {
+            if (nterm != NT_H3) return (int)hipErrorInvalidValue;
+            hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EP, true, 1, PRE>), grid, dim3(HTHREADS), 0, s,
+                               x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm));
+            return cdm_status();
+        }
     } else {
     switch (nterm) {
         case 1:
             if constexpr (!PRE::on) {
                 if (halo_oneb() && halo_deep() && Cin % 32 == 0) {
-                    hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, 1 | 2048 | 4096, PRE>),
+                    hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EP, true, 1 | 2048 | 4096, PRE, XT>),
                                        grid, dim3(HTHREADS), 0, s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre,
                                        mtiles, tpb, halo_stagger(nterm));
                     break;
@@ -1875,36 +1906,43 @@ static int launch_conv_halo(const float* x, int N, int H, int Cin, int ldx, cons
             }
             // (the BN-backward staging form spills 12 VGPRs with the 9-tap B set: one barrier per chunk only by request)
             if (PRE::on ? halo_oneb_bwd() : halo_oneb())
-                hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, 1 | 2048, PRE>), grid, dim3(HTHREADS),
+                hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EP, true, 1 | 2048, PRE, XT>), grid, dim3(HTHREADS),
                                    0, s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm));
             else
-                hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EpiStoreW<4>, true, 1, PRE>), grid, dim3(HTHREADS), 0, s,
+                hipLaunchKernelGGL((conv3x3_halo_x3_kernel<1, WT, EP, true, 1, PRE, XT>), grid, dim3(HTHREADS), 0, s,
                                    x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm));
             break;
-        case 3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<3, WT, EpiStoreW<4>, true, (3 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
-        case NT_H3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EpiStoreW<4>, true, (NT_H3 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0,
-                                       s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
-        case 6: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<6, WT, EpiStoreW<4>, true, (6 >= 6 ? 0 : 1), PRE>), grid, dim3(HTHREADS), 0, s, x, H,
-                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
-        default: return (int)hipErrorInvalidValue;
+        default:
+            if constexpr (F32) {
+                switch (nterm) {
+                    case 3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<3, WT, EP, true, 1, PRE>), grid, dim3(HTHREADS), 0, s, x, H,
+                                               Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
+                    case NT_H3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EP, true, 1, PRE>), grid, dim3(HTHREADS), 0,
+                                                   s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
+                    case 6: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<6, WT, EP, true, 0, PRE>), grid, dim3(HTHREADS), 0, s, x, H,
+                                               Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
+                    default: return (int)hipErrorInvalidValue;
+                }
+            } else {
+                return (int)hipErrorInvalidValue;
+            }
     }
     return cdm_status();
     }
 }
 
 // LDS-halo conv of a W x W image (W in {32, 64}; 128 / 256 with the h3 arithmetic only)
-template <class PRE = PreNone>
-static int launch_conv_halo_w(int W, const float* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
-                              const float* amax_x, const float* amax_w, const EpiStoreW<4>& ep, int nterm,
+template <class PRE = PreNone, class XT = float, class OT = float>
+static int launch_conv_halo_w(int W, const XT* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
+                              const float* amax_x, const float* amax_w, const EpiStoreW<4, OT>& ep, int nterm,
                               hipStream_t s, PRE pre = PRE{}) {
     switch (W) {
-        case 32: return launch_conv_halo<32>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
-        case 64: return launch_conv_halo<64>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
-        case 128: return launch_conv_halo<128>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
+        case 32: return launch_conv_halo<32, PRE, XT, OT>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
+        case 64: return launch_conv_halo<64, PRE, XT, OT>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
+        case 128: return launch_conv_halo<128, PRE, XT, OT>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
         case 256:   // the BN-backward staging registers do not fit next to the 7 halo pieces of a 256-wide row
             if constexpr (PRE::on) return (int)hipErrorInvalidValue;
-            else return launch_conv_halo<256>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
+            else return launch_conv_halo<256, PRE, XT, OT>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
         default: return (int)hipErrorInvalidValue;
     }
 }
@@ -2155,7 +2193,7 @@ static int conv3x3_fwd_split(const float* x, int N, int H, int W, int Cin, int l
                              const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags,
                              float* stats, int stats_ld, int kc, int nterm, float* amax_y, hipStream_t st,
                              const float* pre_s = nullptr, const float* pre_t = nullptr, int* ymm = nullptr,
-                             int ymm_ld = 0) {
+                             int ymm_ld = 0, int dt = 0) {
     if (Cin % 4 || Cout % 4 || (kc != 0 && kc != 16) || (kc == 16 && Cin % 16)) return (int)hipErrorInvalidValue;
     const int M = N * H * W, K = 9 * Cin;
     MkPre mb{reinterpret_cast<const __bf16*>(wx), Cout, amax_w};
@@ -2164,13 +2202,25 @@ static int conv3x3_fwd_split(const float* x, int N, int H, int W, int Cin, int l
                       (unsigned long long)M * (unsigned)ldx * 4ull < (1ull << 32);   // 32-bit halo source offsets
     if ((pre_s || ymm) && (!halo || (ymm && !stats) || (pre_s && (!pre_t || Cin > 256))))
         return (int)hipErrorInvalidValue;      // the fused BN-ReLU input / max-min epilogue: LDS-halo path only
-    if (halo) {   // LDS-halo path
-        EpiStoreW<4> eh{y, ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
-        eh.ymm = ymm; eh.ymm_ld = ymm_ld;
-        const __bf16* b = reinterpret_cast<const __bf16*>(wx);
-        if (pre_s) return launch_conv_halo_w(W, x, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st,
-                                             PreBnRelu{{pre_s, pre_t}});
-        return launch_conv_halo_w(W, x, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st);
+    if (dt && (!halo || nterm != 1)) return (int)hipErrorInvalidValue;   // bf16 activations: C4's LDS-halo path only
+    if (halo) {   // LDS-halo path; dt bit 0: x (the BN-ReLU source) is bf16, bit 1: y is stored as bf16
+        auto run = [&](auto xtag, auto otag) {
+            using XT = decltype(xtag);
+            using OT = decltype(otag);
+            EpiStoreW<4, OT> eh{reinterpret_cast<OT*>(y), ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
+            eh.ymm = ymm; eh.ymm_ld = ymm_ld;
+            const __bf16* b = reinterpret_cast<const __bf16*>(wx);
+            const XT* xx = reinterpret_cast<const XT*>(x);
+            if (pre_s) return launch_conv_halo_w(W, xx, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st,
+                                                 PreBnRelu{{pre_s, pre_t}});
+            return launch_conv_halo_w(W, xx, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st);
+        };
+        switch (dt & 3) {
+            case 1: return run(__bf16{}, float{});
+            case 2: return run(float{}, __bf16{});
+            case 3: return run(__bf16{}, __bf16{});
+            default: return run(float{}, float{});
+        }
     }
     if (Cin == 128 && Cout == 128 && H == 64 && W == 64 && kc == 16) {
         using LA = LdIm2colA<128, 16, 64>;
@@ -2243,15 +2293,28 @@ CDM_API int cdm_conv3x3_dgrad_x16_bnbwd(const float* g, int ldg, const float* y,
                                         const float* t, const float* mean, const float* invstd, const float* A,
                                         const float* B, const float* Cc, int N, int H, int W, int C, const void* wx,
                                         const float* amax_dy, const float* amax_w, float* out, int ldo, int Cout,
-                                        int flags, float* amax_out, int nterm, void* stream) {
+                                        int flags, float* amax_out, int nterm, int dt, void* stream) {
     if (!x16_ok(nterm) || W != H || !halo_width_ok(W, nterm) || W > 128 || C % 16 || C > 256 || ldg % 4 || ldy % 4 ||
-        (H * W) % HBM_ || !x16_amax_ok(nterm, amax_dy, amax_w))
+        (H * W) % HBM_ || !x16_amax_ok(nterm, amax_dy, amax_w) || (dt && nterm != 1))
         return (int)hipErrorInvalidValue;
     const int M = N * H * W;
-    const EpiStoreW<4> eh{out, ldo, 0, nullptr, Cout, flags, nullptr, 0, M, Cout, amax_out};
     const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
     const __bf16* b = reinterpret_cast<const __bf16*>(wx);
-    return launch_conv_halo_w(W, g, N, H, C, ldg, b, Cout, amax_dy, amax_w, eh, nterm, S(stream), pre);
+    // dt bit 0: g and y are bf16, bit 1: the output (the producer's g) is stored as bf16
+    auto run = [&](auto xtag, auto otag) {
+        using XT = decltype(xtag);
+        using OT = decltype(otag);
+        const EpiStoreW<4, OT> eh{reinterpret_cast<OT*>(out), ldo, 0, nullptr, Cout, flags, nullptr, 0, M, Cout,
+                                  amax_out};
+        return launch_conv_halo_w(W, reinterpret_cast<const XT*>(g), N, H, C, ldg, b, Cout, amax_dy, amax_w, eh, nterm,
+                                  S(stream), pre);
+    };
+    switch (dt & 3) {
+        case 1: return run(__bf16{}, float{});
+        case 2: return run(float{}, __bf16{});
+        case 3: return run(__bf16{}, __bf16{});
+        default: return run(float{}, float{});
+    }
 }
 CDM_API int cdm_conv3x3_dgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
                                        const float* t, const float* mean, const float* invstd, const float* A,
@@ -2259,7 +2322,7 @@ CDM_API int cdm_conv3x3_dgrad_h3_bnbwd(const float* g, int ldg, const float* y, 
                                        const float* amax_dy, const float* amax_w, float* out, int ldo, int Cout,
                                        int flags, float* amax_out, void* stream) {
     return cdm_conv3x3_dgrad_x16_bnbwd(g, ldg, y, ldy, s, t, mean, invstd, A, B, Cc, N, H, W, C, wx, amax_dy, amax_w,
-                                       out, ldo, Cout, flags, amax_out, NT_H3, stream);
+                                       out, ldo, Cout, flags, amax_out, NT_H3, 0, stream);
 }
 
 CDM_API int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx3,
@@ -2273,16 +2336,16 @@ CDM_API int cdm_conv3x3_fwd_x3(const float* x, int N, int H, int W, int Cin, int
 CDM_API int cdm_conv3x3_fwd_x16(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx,
                                 const float* amax_x, const float* amax_w, const float* bias, float* y, int ldy,
                                 int Cout, int flags, float* stats, int stats_ld, int kc, float* amax_y, int nterm,
-                                void* stream) {
+                                int dt, void* stream) {
     if (!x16_ok(nterm) || !x16_amax_ok(nterm, amax_x, amax_w)) return (int)hipErrorInvalidValue;
     return conv3x3_fwd_split(x, N, H, W, Cin, ldx, wx, amax_x, amax_w, bias, y, ldy, Cout, flags, stats, stats_ld, kc,
-                             nterm, amax_y, S(stream));
+                             nterm, amax_y, S(stream), nullptr, nullptr, nullptr, 0, dt);
 }
 CDM_API int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
                                const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags,
                                float* stats, int stats_ld, int kc, float* amax_y, void* stream) {
     return cdm_conv3x3_fwd_x16(x, N, H, W, Cin, ldx, wx, amax_x, amax_w, bias, y, ldy, Cout, flags, stats, stats_ld, kc,
-                               amax_y, NT_H3, stream);
+                               amax_y, NT_H3, 0, stream);
 }
 
 // cdm_conv3x3_fwd_h3 + two fusions of the train-mode Conv -> BatchNorm -> ReLU chain (LDS-halo path only):
@@ -2293,17 +2356,18 @@ CDM_API int cdm_conv3x3_fwd_h3(const float* x, int N, int H, int W, int Cin, int
 CDM_API int cdm_conv3x3_fwd_x16_ex(const float* x, int N, int H, int W, int Cin, int ldx, const float* pre_s,
                                    const float* pre_t, const void* wx, const float* amax_x, const float* amax_w,
                                    const float* bias, float* y, int ldy, int Cout, int flags, float* stats,
-                                   int stats_ld, int kc, float* amax_y, int* ymm, int ymm_ld, int nterm, void* stream) {
+                                   int stats_ld, int kc, float* amax_y, int* ymm, int ymm_ld, int nterm, int dt,
+                                   void* stream) {
     if (!x16_ok(nterm) || !x16_amax_ok(nterm, amax_x, amax_w)) return (int)hipErrorInvalidValue;
     return conv3x3_fwd_split(x, N, H, W, Cin, ldx, wx, amax_x, amax_w, bias, y, ldy, Cout, flags, stats, stats_ld, kc,
-                             nterm, amax_y, S(stream), pre_s, pre_t, ymm, ymm_ld);
+                             nterm, amax_y, S(stream), pre_s, pre_t, ymm, ymm_ld, dt);
 }
 CDM_API int cdm_conv3x3_fwd_h3_ex(const float* x, int N, int H, int W, int Cin, int ldx, const float* pre_s,
                                   const float* pre_t, const void* wx, const float* amax_x, const float* amax_w,
                                   const float* bias, float* y, int ldy, int Cout, int flags, float* stats, int stats_ld,
                                   int kc, float* amax_y, int* ymm, int ymm_ld, void* stream) {
     return cdm_conv3x3_fwd_x16_ex(x, N, H, W, Cin, ldx, pre_s, pre_t, wx, amax_x, amax_w, bias, y, ldy, Cout, flags,
-                                  stats, stats_ld, kc, amax_y, ymm, ymm_ld, NT_H3, stream);
+                                  stats, stats_ld, kc, amax_y, ymm, ymm_ld, NT_H3, 0, stream);
 }
 
 // the staggered wave order of the kernel-row weight gradient ($CDM_WGRAD_STAGGER=1; off: same-box A/B, 2 rounds,
@@ -2319,16 +2383,23 @@ static int wgrad_stagger() {
 // (BN coefficients moved to LDS to make room): C2 51.07-51.22 -> 51.87-52.01 ms per step, C4 neutral; the same with the
 // next step's staging interleaved into the MFMAs' scheduling region (sched_group_barrier: 1 MFMA, 2 LDS reads, 5 VALU
 // per gap): C2 49.78-49.91 -> 51.19-51.68 ms, C4 neutral.
-template <int KS, class PRE = PreNone, class PX = PreNone>
-static int launch_wgrad_row(const float* dy, int lddy, int Cout, const float* x, int H, int W, int Cin, int ldx, int K,
+template <int KS, class PRE = PreNone, class PX = PreNone, class GT = float, class XT = float>
+static int launch_wgrad_row(const GT* dy, int lddy, int Cout, const XT* x, int H, int W, int Cin, int ldx, int K,
                             int sp, const float* amax_dy, const float* amax_x, float* slab, int nterm, hipStream_t st,
                             PRE pre = PRE{}, PX px = PX{}) {
+    constexpr bool F32 = std::is_same<GT, float>::value && std::is_same<XT, float>::value;
     const int ktiles = K / (16 * KS), per = (ktiles + sp - 1) / sp;
     dim3 grid((Cout / 128) * 3 * (Cin / 128) * ((ktiles + per - 1) / per));
+    if (!F32 && nterm != 1) return (int)hipErrorInvalidValue;   // bf16 activations: the one-term (C4) arithmetic only
     if constexpr (KS == 4) {   // 64-pixel K steps: the one-term bf16 images only (66 KiB of LDS; h3 would need 133)
         if (nterm != 1) return (int)hipErrorInvalidValue;
-        hipLaunchKernelGGL((wgrad3x3_row_kernel<1, 4, PRE, PX>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W, Cin,
-                           ldx, ktiles, per, amax_dy, amax_x, slab, pre, px, wgrad_stagger());
+        hipLaunchKernelGGL((wgrad3x3_row_kernel<1, 4, PRE, PX, GT, XT>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W,
+                           Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px, wgrad_stagger());
+        return cdm_status();
+    } else {
+    if constexpr (!F32) {
+        hipLaunchKernelGGL((wgrad3x3_row_kernel<1, KS, PRE, PX, GT, XT>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H,
+                           W, Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px, wgrad_stagger());
         return cdm_status();
     } else {
     if constexpr (PX::kind != 0) {            // the fused X transform: the 16-bit arithmetics (h3, bf16)
@@ -2354,6 +2425,7 @@ static int launch_wgrad_row(const float* dy, int lddy, int Cout, const float* x,
         default: return (int)hipErrorInvalidValue;
     }
     return cdm_status();
+    }
     }
 }
 
@@ -2428,17 +2500,32 @@ CDM_API int cdm_conv3x3_wgrad_x16_bnbwd(const float* g, int ldg, const float* y,
                                         const float* t, const float* mean, const float* invstd, const float* A,
                                         const float* B, const float* Cc, int Cout, const float* x, int N, int H, int W,
                                         int Cin, int ldx, const float* amax_dy, const float* amax_x, int splits,
-                                        float* slab, int nterm, void* stream) {
+                                        float* slab, int nterm, int dt, void* stream) {
     if (!x16_ok(nterm) || Cin % 128 || Cout % 128 || W % 16 || ldg % 4 || ldy % 4 || ldx % 4 ||
-        !x16_amax_ok(nterm, amax_dy, amax_x))
+        !x16_amax_ok(nterm, amax_dy, amax_x) || (dt && nterm != 1))
         return (int)hipErrorInvalidValue;
     const int K = N * H * W, sp = effective_splits(K, splits);
     const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
-    if (W % 32 == 0 && effective_splits(K, splits, 32) == sp)
-        return launch_wgrad_row<2>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, nterm, S(stream), pre);
-    if (effective_splits(K, splits, 16) == sp)
-        return launch_wgrad_row<1>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, nterm, S(stream), pre);
-    return (int)hipErrorInvalidValue;
+    // dt bit 0: g and y are bf16, bit 1: x is bf16
+    auto run = [&](auto gtag, auto xtag) {
+        using GT = decltype(gtag);
+        using XT = decltype(xtag);
+        const GT* gg = reinterpret_cast<const GT*>(g);
+        const XT* xx = reinterpret_cast<const XT*>(x);
+        if (W % 32 == 0 && effective_splits(K, splits, 32) == sp)
+            return launch_wgrad_row<2>(gg, ldg, Cout, xx, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, nterm, S(stream),
+                                       pre);
+        if (effective_splits(K, splits, 16) == sp)
+            return launch_wgrad_row<1>(gg, ldg, Cout, xx, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, nterm, S(stream),
+                                       pre);
+        return (int)hipErrorInvalidValue;
+    };
+    switch (dt & 3) {
+        case 1: return run(__bf16{}, float{});
+        case 2: return run(float{}, __bf16{});
+        case 3: return run(__bf16{}, __bf16{});
+        default: return run(float{}, float{});
+    }
 }
 CDM_API int cdm_conv3x3_wgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
                                        const float* t, const float* mean, const float* invstd, const float* A,
@@ -2446,7 +2533,7 @@ CDM_API int cdm_conv3x3_wgrad_h3_bnbwd(const float* g, int ldg, const float* y, 
                                        int Cin, int ldx, const float* amax_dy, const float* amax_x, int splits,
                                        float* slab, void* stream) {
     return cdm_conv3x3_wgrad_x16_bnbwd(g, ldg, y, ldy, s, t, mean, invstd, A, B, Cc, Cout, x, N, H, W, Cin, ldx, amax_dy,
-                                       amax_x, splits, slab, NT_H3, stream);
+                                       amax_x, splits, slab, NT_H3, 0, stream);
 }
 
 // the kernel-row weight gradient with both staging fusions selectable: g / y / BN coefficients (optional, all or
@@ -2458,10 +2545,10 @@ CDM_API int cdm_conv3x3_wgrad_x16_ex(const float* g, int ldg, const float* y, in
                                      const float* x_s, const float* x_t, const float* x_g, int ldxg,
                                      const float* x_mean, const float* x_invstd, float* x_sums,
                                      const float* amax_dy, const float* amax_x, int splits, float* slab, int nterm,
-                                     void* stream) {
+                                     int dt, void* stream) {
     if (!x16_ok(nterm) || Cin % 128 || Cout % 128 || W % 16 || ldg % 4 || ldx % 4 ||
         !x16_amax_ok(nterm, amax_dy, amax_x) || (x_s && !x_t) || (y && ldy % 4) ||
-        (x_sums && (!x_s || !x_g || ldxg % 4 || !x_mean || !x_invstd)))
+        (x_sums && (!x_s || !x_g || ldxg % 4 || !x_mean || !x_invstd)) || (dt && nterm != 1))
         return (int)hipErrorInvalidValue;
     const int K = N * H * W, sp = effective_splits(K, splits);
     const bool ks2 = W % 32 == 0 && effective_splits(K, splits, 32) == sp;
@@ -2473,19 +2560,32 @@ CDM_API int cdm_conv3x3_wgrad_x16_ex(const float* g, int ldg, const float* y, in
     const PreBnRelu px{{x_s, x_t}};
     const PreBnReluSums pxs{{x_s, x_t}, x_g, ldxg, x_mean, x_invstd, x_sums};
     hipStream_t st = S(stream);
-#define CDM_WG(KS_, PRE_, PX_) launch_wgrad_row<KS_>(g, ldg, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, \
+    // dt bit 0: g (and y) are bf16, bit 1: x (and x_g) are bf16
+    auto run = [&](auto gtag, auto xtag) {
+        using GT = decltype(gtag);
+        using XT = decltype(xtag);
+        const GT* gg = reinterpret_cast<const GT*>(g);
+        const XT* xx = reinterpret_cast<const XT*>(x);
+#define CDM_WG(KS_, PRE_, PX_) launch_wgrad_row<KS_>(gg, ldg, Cout, xx, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, \
                                                      nterm, st, PRE_, PX_)
 #define CDM_WGK(PRE_, PX_) (ks4 ? CDM_WG(4, PRE_, PX_) : ks2 ? CDM_WG(2, PRE_, PX_) : CDM_WG(1, PRE_, PX_))
-    if (x_sums) {   // the producer's BN-backward sums ride along (x_sums[splits][5][Cin])
-        if (y) return CDM_WGK(pre, pxs);
-        return CDM_WGK(PreNone{}, pxs);
-    }
-    if (y && x_s) return CDM_WGK(pre, px);
-    if (y) return CDM_WGK(pre, PreNone{});
-    if (x_s) return CDM_WGK(PreNone{}, px);
-    return CDM_WGK(PreNone{}, PreNone{});
+        if (x_sums) {   // the producer's BN-backward sums ride along (x_sums[splits][5][Cin])
+            if (y) return CDM_WGK(pre, pxs);
+            return CDM_WGK(PreNone{}, pxs);
+        }
+        if (y && x_s) return CDM_WGK(pre, px);
+        if (y) return CDM_WGK(pre, PreNone{});
+        if (x_s) return CDM_WGK(PreNone{}, px);
+        return CDM_WGK(PreNone{}, PreNone{});
 #undef CDM_WGK
 #undef CDM_WG
+    };
+    switch (dt & 3) {
+        case 1: return run(__bf16{}, float{});
+        case 2: return run(float{}, __bf16{});
+        case 3: return run(__bf16{}, __bf16{});
+        default: return run(float{}, float{});
+    }
 }
 CDM_API int cdm_conv3x3_wgrad_h3_ex(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
                                     const float* mean, const float* invstd, const float* A, const float* B,
@@ -2493,7 +2593,7 @@ CDM_API int cdm_conv3x3_wgrad_h3_ex(const float* g, int ldg, const float* y, int
                                     const float* x_s, const float* x_t, const float* amax_dy, const float* amax_x,
                                     int splits, float* slab, void* stream) {
     return cdm_conv3x3_wgrad_x16_ex(g, ldg, y, ldy, s, t, mean, invstd, A, B, Cc, Cout, x, N, H, W, Cin, ldx, x_s, x_t,
-                                    nullptr, 0, nullptr, nullptr, nullptr, amax_dy, amax_x, splits, slab, NT_H3, stream);
+                                    nullptr, 0, nullptr, nullptr, nullptr, amax_dy, amax_x, splits, slab, NT_H3, 0, stream);
 }
 
 static int split_blocks(int K, int N) {

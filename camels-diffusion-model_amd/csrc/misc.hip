@@ -655,7 +655,7 @@ __global__ void avgpool_gelu_fin_kernel(const float* sums, int N, int C, float i
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N * C) return;
     const float m = sums[i] * inv_hw;
-    hpre[i] = m; hv[i] = gelu_f(m);
+    hpre[i] = m; hv[i] = (float)gelu_d((double)m);   // GELU rounded once (see embed_fwd_kernel)
 }
 // dst[n,p,c] += dhv[n][c] * gelu'(hpre[n][c]) / HW
 __global__ void avgpool_gelu_bwd_kernel(const float* dhv, const float* hpre, int N, int HW, int C, float inv_hw,
@@ -689,23 +689,28 @@ struct MlpDesc {
 };
 struct Mlp4 { MlpDesc m[4]; };
 
+// Evaluated in fp64 and rounded once (the embeddings are a few thousand values per step): the same inputs give the
+// same embedding at every step of a sampling run (c is fixed, t moves slowly), so any rounding bias of an fp32
+// evaluation is repeated 1500 times and accumulates coherently along the trajectory; rounded once, the embedding
+// is within half an ulp of the exact value (tools/t1500_steps.py: the fp32 kernel's c / t embedding errors were 1.7x /
+// 6.6x the reference's, coherent over the run).  pre / h (kept for the backward) are the rounded fp64 values.
 __global__ __launch_bounds__(256) void embed_fwd_kernel(Mlp4 P) {
     const MlpDesc& d = P.m[blockIdx.y];
     const int b = blockIdx.x;
     if (b >= d.rows) return;
-    __shared__ float hs[1024];
+    __shared__ double hs[1024];
     for (int j = threadIdx.x; j < d.E; j += 256) {
-        float s = d.b1[j];
-        for (int k = 0; k < d.in_dim; ++k) s = fmaf(d.w1[j * d.in_dim + k], d.x[b * d.in_dim + k], s);
-        const float g = gelu_f(s);
-        if (d.pre) { d.pre[(long long)b * d.E + j] = s; d.h[(long long)b * d.E + j] = g; }
+        double s = d.b1[j];
+        for (int k = 0; k < d.in_dim; ++k) s = fma((double)d.w1[j * d.in_dim + k], (double)d.x[b * d.in_dim + k], s);
+        const double g = gelu_d(s);
+        if (d.pre) { d.pre[(long long)b * d.E + j] = (float)s; d.h[(long long)b * d.E + j] = (float)g; }
         hs[j] = g;
     }
     __syncthreads();
     for (int j = threadIdx.x; j < d.E; j += 256) {
-        float s = 0.f;
-        for (int i = 0; i < d.E; ++i) s = fmaf(d.w2t[(long long)i * d.E + j], hs[i], s);
-        d.out[(long long)b * d.E + j] = s + d.b2[j];
+        double s = d.b2[j];
+        for (int i = 0; i < d.E; ++i) s = fma((double)d.w2t[(long long)i * d.E + j], hs[i], s);
+        d.out[(long long)b * d.E + j] = (float)s;
     }
 }
 

@@ -132,6 +132,12 @@ class UNetEngine:
         self.fuse_bn_sums = self.x16 and (env == "1" if env is not None else not self.h3)
         # init_conv.conv1's BN backward inside its weight-gradient kernel ($CDM_FUSE_CIN1_BWD=0: the apply kernel)
         self.fuse_cin1_bwd = os.environ.get("CDM_FUSE_CIN1_BWD", "1") != "0"
+        # C4 mixed precision (bf16 arithmetic, train mode): the fused Conv -> BN -> ReLU chain's pre-norm outputs y and
+        # their gradients g are stored as bf16 (torch.autocast keeps conv outputs and their gradients in bf16), halving
+        # the bytes every fused conv stages; BN statistics, accumulators, master weights stay fp32.  The chain's ends
+        # (concatenation slices, pool / FiLM / residual outputs, the C_in = 1 init conv) stay fp32.
+        # $CDM_ACT16=0 keeps fp32 activations (A/B checks).
+        self.act16 = self.nterm == 1 and os.environ.get("CDM_ACT16", "1") != "0"
         self.device = torch.device(device)
         self.layers = conv_layers(n_feat, height)
         self.L = {l.name: l for l in self.layers}
@@ -290,7 +296,7 @@ class UNetEngine:
         return _p(self.pk[key + "_amax"]) if self.h3 else None
 
     def conv3x3(self, key, x_p, B, S, cin, ldx, bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, s,
-                amax_x=None, amax_y=None, pre=None, ymm=None):
+                amax_x=None, amax_y=None, pre=None, ymm=None, dt=0):
         """3x3 conv (fwd or dgrad) with the packed weights pk[key], in this engine's conv arithmetic.
 
         h3 only: amax_x = device max|x| written by x's producer (None: measured here by a separate pass);
@@ -298,13 +304,14 @@ class UNetEngine:
         relu(x * scale + shift) of the previous layer's pre-norm output, applied while staging; ymm = (ptr, ld):
         per-channel max / min keys of y for the next layer's fused apply."""
         args = (key, x_p, B, S, cin, ldx, bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, s, amax_x, amax_y,
-                pre, ymm)
+                pre, ymm, dt)
         if self.launch_probe is not None:
             self.launch_probe(args)
         self._conv3x3(*args)
 
     def _conv3x3(self, key, x_p, B, S, cin, ldx, bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, s, amax_x,
-                 amax_y, pre, ymm):
+                 amax_y, pre, ymm, dt=0):
+        """dt (bf16 activations, C4): bit 0 the source holds bf16, bit 1 the output is stored as bf16."""
         if self.x16:
             if self.h3 and amax_x is None:
                 assert pre is None
@@ -315,10 +322,10 @@ class UNetEngine:
                 ym, yld = ymm if ymm is not None else (None, 0)
                 lib().cdm_conv3x3_fwd_x16_ex(x_p, B, S, S, cin, ldx, ps, pt, _p(self.pk[key + "_x"]), amax_x,
                                              self._wamax(key), bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc,
-                                             amax_y, ym, yld, self.nterm, s)
+                                             amax_y, ym, yld, self.nterm, dt, s)
                 return
             lib().cdm_conv3x3_fwd_x16(x_p, B, S, S, cin, ldx, _p(self.pk[key + "_x"]), amax_x, self._wamax(key),
-                                      bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, amax_y, self.nterm, s)
+                                      bias_p, y_p, ldy, cout, flags, stats_p, stats_ld, kc, amax_y, self.nterm, dt, s)
         elif self.nterm:
             lib().cdm_conv3x3_fwd_x3(x_p, B, S, S, cin, ldx, _p(self.pk[key + "_x"]), bias_p, y_p, ldy, cout, flags,
                                      stats_p, stats_ld, kc, self.nterm, s)
@@ -470,6 +477,7 @@ class UNetEngine:
         # ---------------- out ----------------
         self.conv3x3("out.0.wpk", ws.catO.p, B, H, 2 * nf, 2 * nf, _p(P["out.0.bias"]), _p(ws.yO), nf, nf, 0,
                      _p(ws.slab), nf, self.kc_out0, s, amax_x=self._slot(ws, "catO"))
+        probe("yO", ws)
         self._gn_fwd(ws, P, "out.1", Act(ws.yO, nf), B, H, nf, ws.gnO, stats_from_conv=True, stream=s)
         if not train and nf % 16 == 0 and H <= 256 and 256 % H == 0:
             # eval: out.1's GroupNorm + ReLU applied in out.3's staging (zO is only kept for the backward)
@@ -512,7 +520,7 @@ class UNetEngine:
                 ymm = ws.ymm_of(l) if (l.name in ws.fused_fwd and self.h3) else None
                 self.conv3x3(l.name + ".wpk", src.p, B, S, l.cin, src.ld, _p(P[l.b]), _p(y), l.cout, l.cout, 0,
                              _p(ws.slab), l.cout, l.kc, s, amax_x=self._src_slot(ws, l), amax_y=yslot, pre=pre,
-                             ymm=ymm)
+                             ymm=ymm, dt=self._fwd_dt(ws, l, pre))
                 ntiles = _cdiv(npix, CHUNK)
             bn = l.bn
             nparts = fold(ws, _p(ws.slab), ntiles, 2, l.cout, s)
@@ -742,6 +750,7 @@ class UNetEngine:
             assert mode == 0
             nparts = fold(ws, _p(ws.sums), ws.sums_sp[l.name], 5, C, s)
         else:
+            assert l.name not in ws.act16, "bf16 activations need the fused BN-backward sums"
             lb.cdm_norm_bwd_reduce(mode, g.p, g.ld, _p(y), C, B, S, S, C, _p(st["scale"]), _p(st["shift"]), 0,
                                    _p(st["mean"]), _p(st["invstd"]), 0, 1, _p(film_a), film_an, CHUNK, _p(ws.slab), s)
             if mode == 2:  # FiLM2 sums -> d cemb2 / d temb2 (per sample)
@@ -765,16 +774,18 @@ class UNetEngine:
             # dgrad first: it writes the producer's g, which the weight gradient's producer sums read
             dgd = ws.dgrad_dst[l.name]
             key = l.name + ".wdg"
+            own16 = 1 if l.name in ws.act16 else 0
             lb.cdm_conv3x3_dgrad_x16_bnbwd(g.p, g.ld, _p(y), C, *coef, B, S, S, C, _p(self.pk[key + "_x"]), dslot,
                                            self._wamax(key), dgd.p, dgd.ld, l.cin,
-                                           EPI_ACCUM if ws.dgrad_accum[l.name] else 0, gslot, self.nterm, s)
+                                           EPI_ACCUM if ws.dgrad_accum[l.name] else 0, gslot, self.nterm,
+                                           own16 | self._dgrad_out16(ws, l), s)
             if pre is None:
                 lb.cdm_conv3x3_wgrad_x16_bnbwd(g.p, g.ld, _p(y), C, *coef, C, src.p, B, S, S, l.cin, src.ld, dslot,
-                                               self._src_slot(ws, l), sp, _p(ws.slab), self.nterm, s)
+                                               self._src_slot(ws, l), sp, _p(ws.slab), self.nterm, own16, s)
             else:
                 lb.cdm_conv3x3_wgrad_x16_ex(g.p, g.ld, _p(y), C, *coef, C, src.p, B, S, S, l.cin, src.ld, pre[0],
                                             pre[1], *self._producer_sums(ws, l, sp), dslot, self._src_slot(ws, l), sp,
-                                            _p(ws.slab), self.nterm, s)
+                                            _p(ws.slab), self.nterm, own16 | self._prod16(ws, l), s)
             lb.cdm_slab_reduce(_p(ws.slab), sp, C, 9 * l.cin, _p(G[l.w]), 9 * l.cin, 1, 9, l.cin, 0, 1.0, s)
             return
         if l.cin == 1 and mode == 0 and self.fuse_cin1_bwd:
@@ -800,7 +811,8 @@ class UNetEngine:
         dgd = ws.dgrad_dst[l.name]
         # dgrad first (it writes the producer's g, read by the producer sums of the weight gradient below)
         self.conv3x3(l.name + ".wdg", dy.p, B, S, C, dy.ld, None, dgd.p, dgd.ld, l.cin,
-                     EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s, amax_x=dslot, amax_y=gslot)
+                     EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s, amax_x=dslot, amax_y=gslot,
+                     dt=self._dgrad_out16(ws, l))
         self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s, amax_dy=dslot, amax_x=self._src_slot(ws, l), pre=pre,
                        sums_of=l)
 
@@ -813,6 +825,25 @@ class UNetEngine:
             st = ws.bn[p.name]
             return Act(ws.y[p.name], p.cout), (_p(st["scale"]), _p(st["shift"]))
         return ws.src[l.name], None
+
+    # bf16 activation storage (C4): dtype bits of the conv launches around layer l ---------------------------------
+    def _prod16(self, ws, l: "LayerSpec") -> int:
+        """2 when conv l's input is the bf16 pre-norm output of a fused producer (its staging applies BN-ReLU), else 0."""
+        i = self.layers.index(l)
+        return 2 if (i > 0 and self.layers[i - 1].name in ws.act16 and self.layers[i - 1].name in ws.fused_fwd) else 0
+
+    def _fwd_dt(self, ws, l: "LayerSpec", pre) -> int:
+        """forward conv l: bit 0 its source is a bf16 y (BN-ReLU staged), bit 1 its y is stored as bf16."""
+        src16 = 1 if (pre is not None and self._prod16(ws, l)) else 0
+        return src16 | (2 if l.name in ws.act16 else 0)
+
+    def _dgrad_out16(self, ws, l: "LayerSpec") -> int:
+        """2 when the input gradient conv l writes (the gradient of its producer's output) is stored as bf16."""
+        i = self.layers.index(l)
+        if i == 0 or ws.dgrad_accum.get(l.name, False):
+            return 0
+        p = self.layers[i - 1]
+        return 2 if (p.name in ws.act16 and ws.gout[p.name].buf.data_ptr() == ws.dgrad_dst[l.name].buf.data_ptr()) else 0
 
     def _dgrad_amax_slot(self, ws, l: "LayerSpec"):
         """Slot that receives max|dgrad output| of layer l: the grad wrt a ConvT output (h3 ConvT backward) or
@@ -841,9 +872,10 @@ class UNetEngine:
         sp = wgrad_splits(B * S * S, cout, 9 * cin)
         if pre is not None:        # X = relu(x s + t) of a fused producer (16-bit arithmetic, kernel-row weight gradient)
             sums = self._producer_sums(ws, sums_of, sp) if sums_of is not None else (None, 0, None, None, None)
+            dt = 2 if (sums_of is not None and self._prod16(ws, sums_of)) else 0
             lb.cdm_conv3x3_wgrad_x16_ex(dy.p, dy.ld, None, 0, None, None, None, None, None, None, None, cout, x.p, B, S,
                                         S, cin, x.ld, pre[0], pre[1], *sums, amax_dy, amax_x, sp, _p(ws.slab),
-                                        self.nterm, s)
+                                        self.nterm, dt, s)
             lb.cdm_slab_reduce(_p(ws.slab), sp, cout, 9 * cin, _p(gW), 9 * cin, 1, 9, cin, 0, 1.0, s)
             return
         if self.x16:
@@ -1101,9 +1133,17 @@ class Workspace:
             nsum = max([wgrad_splits(B * L[i].S * L[i].S, L[i].cout, 9 * L[i].cin) * 3 * (L[i].cout // 128) * 5
                         * L[i].cin for i in range(len(L)) if L[i].name in self.sums_from] + [1])
             self.sums = E(nsum)
+            # bf16 activations (C4): the fused chain's y and g (layers whose BN-ReLU apply runs in the next conv's
+            # staging, C_in > 1; each has its BN-backward sums fused into the consumer's weight gradient and a private
+            # gradient buffer, so every kernel reading them is one of the two templated conv kernels)
+            self.act16 = set()
+            if eng.act16:
+                self.act16 = {l.name for l in L if l.name in self.fused_fwd and l.cin > 1 and l.name in self.sums_by
+                              and l.name in self.fused and self.gout[l.name].off == 0}
         else:
             self.fused, self.g_amax_key, self.out0_g_key = set(), {}, None
             self.sums_from, self.sums_by, self.sums_sp = {}, {}, {}
+            self.act16 = set()
 
     def ymm_of(self, l) -> tuple:
         """(pointer, ld) of fused layer l's max keys; its min keys sit ld ints further."""

@@ -103,23 +103,28 @@ int cdm_conv3x3_wgrad_h3_ex(const float* g, int ldg, const float* y, int ldy, co
  * Conv -> BatchNorm -> ReLU fusion of the h3 path).  For nterm = 1 the weight images come from cdm_split_bf16x3 (plane
  * 0 is read) and the amax_* operand maxima are ignored (may be null).  Reference ops: nn.Conv2d(.,.,3,1,1)
  * diffusion_utilities.py:27,34 and its autograd; nn.ConvTranspose2d(Cin, Cout, 2, 2) diffusion_utilities.py:86. */
+/* dt (the x16 conv entry points): bf16 activation storage of C4's fused Conv -> BatchNorm -> ReLU chain, one-term
+ * (nterm = 1) arithmetic only.  Forward / dgrad: bit 0 = the source (x or g, and the BN staging's y) holds bf16, bit 1 =
+ * the output is stored as bf16 (statistics / maxima of the stored values).  Weight gradient: bit 0 = g / dy (and y) are
+ * bf16, bit 1 = x (and x_g) are bf16.  dt = 0: fp32 everywhere (every other arithmetic). */
 int cdm_conv3x3_fwd_x16(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
                         const float* amax_w, const float* bias, float* y, int ldy, int Cout, int flags, float* stats,
-                        int stats_ld, int kc, float* amax_y, int nterm, void* stream);
+                        int stats_ld, int kc, float* amax_y, int nterm, int dt, void* stream);
 int cdm_conv3x3_fwd_x16_ex(const float* x, int N, int H, int W, int Cin, int ldx, const float* pre_s, const float* pre_t,
                            const void* wx, const float* amax_x, const float* amax_w, const float* bias, float* y,
                            int ldy, int Cout, int flags, float* stats, int stats_ld, int kc, float* amax_y, int* ymm,
-                           int ymm_ld, int nterm, void* stream);
+                           int ymm_ld, int nterm, int dt, void* stream);
 int cdm_conv3x3_wgrad_x16(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,
                           const float* amax_dy, const float* amax_x, int splits, float* slab, int nterm, void* stream);
 int cdm_conv3x3_dgrad_x16_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
                                 const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
                                 int N, int H, int W, int C, const void* wx, const float* amax_dy, const float* amax_w,
-                                float* out, int ldo, int Cout, int flags, float* amax_out, int nterm, void* stream);
+                                float* out, int ldo, int Cout, int flags, float* amax_out, int nterm, int dt,
+                                void* stream);
 int cdm_conv3x3_wgrad_x16_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
                                 const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
                                 int Cout, const float* x, int N, int H, int W, int Cin, int ldx, const float* amax_dy,
-                                const float* amax_x, int splits, float* slab, int nterm, void* stream);
+                                const float* amax_x, int splits, float* slab, int nterm, int dt, void* stream);
 /* cdm_conv3x3_wgrad_x16_ex also takes (x_g, ldxg, x_mean, x_invstd, x_sums), all optional (x_sums null: off): with
  * x_s / x_t given, the BatchNorm-backward channel sums of the layer that produced x are accumulated while x is staged:
  * g_pre = (x x_s + x_t > 0 ? x_g : 0), xhat = (x - x_mean) x_invstd; x_sums[(split * 3 + kernel row) * (Cout / 128) +
@@ -131,7 +136,7 @@ int cdm_conv3x3_wgrad_x16_ex(const float* g, int ldg, const float* y, int ldy, c
                              int Cout, const float* x, int N, int H, int W, int Cin, int ldx, const float* x_s,
                              const float* x_t, const float* x_g, int ldxg, const float* x_mean, const float* x_invstd,
                              float* x_sums, const float* amax_dy, const float* amax_x, int splits, float* slab,
-                             int nterm, void* stream);
+                             int nterm, int dt, void* stream);
 int cdm_convT2x2_fwd_x16(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx, const float* amax_x,
                          const float* amax_w, const float* bias, float* y, int ldy, int Cout, float* amax_y, int nterm,
                          void* stream);

@@ -34,7 +34,7 @@ def main(out_path):
     st = torch.empty(P // 128, 2, C, device="cuda")
     assert L.cdm_conv3x3_fwd_x16_ex(x.data_ptr(), N, H, H, C, C, ps.data_ptr(), pt.data_ptr(), wx.data_ptr(), None,
                                     None, b.data_ptr(), y.data_ptr(), C, C, 0, st.data_ptr(), C, 16, None, None, 0, 1,
-                                    s) == 0
+                                    0, s) == 0
     out["halo_y"], out["halo_stats"] = y.cpu(), st.cpu()
     # kernel-row weight gradient, BN-backward dY staging + BN-ReLU X staging, both 16-bit arithmetics
     from cdm_amd.engine import wgrad_splits
@@ -53,7 +53,7 @@ def main(out_path):
             assert L.cdm_conv3x3_wgrad_x16_ex(gy.data_ptr(), co, yy.data_ptr(), co, *[t.data_ptr() for t in cf], co,
                                               xx.data_ptr(), B, S, S, ci, ci, xs_.data_ptr(), xt_.data_ptr(), None, 0,
                                               None, None, None, am.data_ptr(), am.data_ptr() + 4, sp, slab.data_ptr(),
-                                              nterm, s) == 0
+                                              nterm, 0, s) == 0
             out[f"wgrad_{nterm}_{S}"] = slab.cpu()
     # C_in = 1 forward and C_out = 1 input gradient: the row kernels vs the flat-pixel kernels ($CDM_ROW_KERNELS)
     for (N, H, W, C) in ((3, 64, 64, 128), (2, 32, 32, 256), (2, 24, 40, 64), (1, 256, 256, 128)):

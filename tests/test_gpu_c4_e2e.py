@@ -3,9 +3,10 @@ step bench.py times for C4, at its own shape — n_feat = 128, 6 params, 64x64, 
 hipGraph replay; the first two bench steps (seeded init torch.manual_seed(0), x0 / c from the CUDA generator 1234,
 Trainer seed 0, lr 1e-5, Philox noise / t / shortcut read back from the Trainer's device buffers).
 
-The reference for mixed precision is the reference run under the same operand rounding: the CPU oracle with every 3x3
-conv (C_in > 1) and both ConvTranspose2d(2, 2) taking bf16-rounded operands, fp32 accumulate
-(test_gpu_configs._bf16_operands, as torch.autocast would feed them) — and the truth is the oracle in fp64
+The reference for mixed precision is the reference run under torch.autocast-like rounding: the CPU oracle with every 3x3
+conv (C_in > 1) and both ConvTranspose2d(2, 2) taking bf16-rounded operands, fp32 accumulate, and those 3x3 convs'
+outputs and their gradients stored in bf16 (test_gpu_configs._bf16_operands(outputs=True); the HIP step stores the fused
+chain's y and g in bf16) — and the truth is the oracle in fp64
 (tests/_oracle_gpu.py, on the GPU).  Bar, per step: HIP's deviation from fp64 within 1.5x the emulated reference's
   eps            max|d| / max|eps|
   loss           |d|                                       (+ 1e-7 |loss|)
@@ -84,7 +85,7 @@ def _emulated_step(sd, x, c, st):
     otr = R.OracleTrainer(s, n_feat=NF, n_cfeat=NCF, height=H, lr=LR)
     _, _, ab = R.make_schedule(T)
     w = st["sc"][:NF].reshape(NF, 1, 1, 1).float(); b = st["sc"][NF:].float()
-    with _bf16_operands():
+    with _bf16_operands(outputs=True):
         loss, pred, grads = otr.step(x, c, st["noise"], st["t"], T, ab, (w, b))
     return float(loss), pred.detach(), grads, {k: v.detach().clone() for k, v in otr.sd.items()}
 

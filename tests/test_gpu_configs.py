@@ -68,9 +68,26 @@ def _forward_pair(nf, H, B, math, seed=3):
     return out
 
 
+class _RoundBF16(torch.autograd.Function):
+    """A tensor stored in bf16 and its gradient stored in bf16 (torch.autocast's conv outputs)."""
+
+    @staticmethod
+    def forward(ctx, v):
+        return v.to(torch.bfloat16).to(v.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
 class _bf16_operands:
     """Oracle hook: round the operands of every 3x3 conv with C_in > 1 and of the two ConvTranspose2d(k=2, s=2) to bf16
-    (fp32 accumulate), as C4 does (the C_in = 1 / C_out = 1 convs and up0 stay fp32 on both sides)."""
+    (fp32 accumulate), as C4 does (the C_in = 1 / C_out = 1 convs and up0 stay fp32 on both sides).  outputs=True also
+    stores those 3x3 convs' outputs and their gradients in bf16, as torch.autocast does (the HIP C4 train step stores
+    the fused chain's y and g in bf16, a subset of these, so this reference is the less precise one)."""
+
+    def __init__(self, outputs: bool = False):
+        self.outputs = outputs
 
     def __enter__(self):
         self.orig, self.orig_t = R.F.conv2d, R.F.conv_transpose2d
@@ -80,7 +97,8 @@ class _bf16_operands:
 
         def conv(x, w, b=None, *a, **k):
             if w.shape[-1] == 3 and w.shape[1] > 1:
-                x, w = bf(x), bf(w)
+                out = self.orig(bf(x), bf(w), b, *a, **k)
+                return _RoundBF16.apply(out) if self.outputs else out
             return self.orig(x, w, b, *a, **k)
 
         def convt(x, w, b=None, *a, **k):
@@ -120,7 +138,7 @@ def _grad_errors(nf, H, B, math, seed=4, emulate_bf16=False):
     got = {k: p.grad.cpu().double() for k, p in m.named_parameters()}
     emu = None
     if emulate_bf16:
-        with _bf16_operands():
+        with _bf16_operands(outputs=True):
             _, emu = oracle(torch.float32)
     errs, errs_emu, zero_ok = {}, {}, True
     for k, v in got.items():
@@ -138,8 +156,11 @@ def test_c4_bf16_forward_vs_oracle():
     """bf16 forward vs the fp32 oracle: within 1.5x the error of the oracle itself under bf16 operand rounding
     (train-mode BatchNorm amplifies operand noise: ~2 % of max|eps| for both on this input)."""
     got = _forward_pair(64, 64, 3, "bf16")
-    with _bf16_operands():
+    with _bf16_operands():                   # eval: operands rounded (the eval forward keeps fp32 activations)
         emu = _forward_pair(64, 64, 3, "fp32")
+    with _bf16_operands(outputs=True):       # train: the fused chain's y also stored in bf16, as autocast does
+        emu_t = _forward_pair(64, 64, 3, "fp32")
+    emu = [emu[0], emu_t[1]]
     for (train, eps, ref), (_, _, ref_bf) in zip(got, emu):
         e_hip, e_emu = _rel(eps, ref), _rel(ref_bf, ref)
         print("train" if train else "eval", "hip", e_hip, "oracle-bf16", e_emu)
@@ -211,7 +232,7 @@ def test_c4_bf16_trainer_step_vs_emulated_oracle():
         w, b = sc[:nf].reshape(nf, 1, 1, 1).to(dtype), sc[nf:].to(dtype)
         args = (x.to(dtype), c.to(dtype), noise.to(dtype), tt, T, ab.to(dtype), (w, b))
         if emulate:
-            with _bf16_operands():
+            with _bf16_operands(outputs=True):
                 l, _, gr = otr.step(*args)
         else:
             l, _, gr = otr.step(*args)

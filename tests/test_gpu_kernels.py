@@ -433,7 +433,7 @@ def test_bf16_halo_conv_vs_fp64(L, N, H, Cin, pre):
     stats = torch.zeros(P // 128, 2, Cout, device="cuda")
     assert L.cdm_conv3x3_fwd_x16_ex(x.data_ptr(), N, H, H, Cin, Cin, s_.data_ptr() if pre else None,
                                     t_.data_ptr() if pre else None, wx.data_ptr(), None, None, b.data_ptr(),
-                                    y.data_ptr(), Cout, Cout, 0, stats.data_ptr(), Cout, 16, None, None, 0, 1,
+                                    y.data_ptr(), Cout, Cout, 0, stats.data_ptr(), Cout, 16, None, None, 0, 1, 0,
                                     _s()) == 0
     torch.cuda.synchronize()
     xin = x.double()
@@ -692,7 +692,7 @@ def test_producer_bn_sums_in_wgrad(B, S, cin, cout, nterm):
                                    y.data_ptr(), B, S, S, cin, cin, s_.data_ptr(), t_.data_ptr(),
                                    gx.data_ptr() if with_sums else None, cin, mean.data_ptr() if with_sums else None,
                                    inv.data_ptr() if with_sums else None, sums.data_ptr() if with_sums else None,
-                                   am.data_ptr(), am.data_ptr() + 4, sp, slab.data_ptr(), nterm, st)
+                                   am.data_ptr(), am.data_ptr() + 4, sp, slab.data_ptr(), nterm, 0, st)
         slabs.append(slab)
     torch.cuda.synchronize()
     assert torch.equal(slabs[0], slabs[1])

@@ -126,16 +126,13 @@ def _moments(tr):
     return m, v
 
 
-@pytest.mark.parametrize("math", ["h3", "x6", "fp32"])
+@pytest.mark.parametrize("math", ["h3"])
 def test_trainer_matches_reference_training_loop(math):
-    """Trainer (inject mode, eager) through three reference loop iterations incl. the per-epoch LR decay.
-
-    Run under the shipped arithmetic h3 and under x6 / fp32.  Only h3 (the default, the one bench.py times) is held
-    to the 3-step trajectory bar after step 0: on this input x6 and fp32 flip one ReLU/MaxPool kink in step 0 that
-    neither the reference nor h3 flip (down1.model.0.conv1 gradients 1.35e-2 rel L2 off the fp64 oracle, median
-    1.2e-6 — inside the step-0 gradient bar), and Adam turns that flip into a 0.16 lr RMS parameter deviation after
-    step 1 (measured on the GPU box).  Every arithmetic keeps the bit-exact Adam check, the step-0 gradient, loss and
-    parameter bars and the running-statistics bar on every step."""
+    """Trainer (inject mode, eager) through three reference loop iterations incl. the per-epoch LR decay, under the
+    shipped arithmetic h3 (the one bench.py times), every bar on every step.  (Round 4: the x6 / fp32
+    parametrisations, which flip one ReLU / MaxPool kink on this golden input in step 0 and needed waivers after it,
+    were removed: test_trainer_three_steps_all_arithmetics holds all three arithmetics to the same bars without
+    waivers on a kink-free input.)"""
     from cdm_amd import Trainer
     fx = np.load(os.path.join(GOLD, "train_nf8.npz"))
     base = np.load(os.path.join(GOLD, "model_nf8.npz"))
@@ -196,7 +193,7 @@ def test_trainer_matches_reference_training_loop(math):
         ref_loss_err = abs(float(fx[f"s{k}_loss"]) - loss64)
         # step 0: the reference's own fp32 error (+1e-5 rel); later steps: 1e-4 rel (a ReLU / MaxPool kink flipped in
         # an earlier step's gradient moves the parameters the loss is evaluated at)
-        assert (math != "h3" and k > 0) or abs(loss - loss64) <= 3 * ref_loss_err + (1e-5 if k == 0 else 1e-4) * abs(loss64), \
+        assert abs(loss - loss64) <= 3 * ref_loss_err + (1e-5 if k == 0 else 1e-4) * abs(loss64), \
             (loss, loss64, float(fx[f"s{k}_loss"]))
         got = {n: post[n] for n in names}
         h_rms, h_p99, h_max = _dev_stats(got, sd64, keep, lr0)
@@ -207,8 +204,7 @@ def test_trainer_matches_reference_training_loop(math):
                        loss_err=abs(loss - loss64), loss_err_ref32=ref_loss_err, param_dev_lr_rms=h_rms,
                        param_dev_lr_p99=h_p99, param_dev_lr_rms_ref32=r_rms, param_dev_lr_p99_ref32=r_p99,
                        adam_exact_frac=frac_r)
-        if math == "h3" or k == 0:
-            assert h_rms <= 3 * r_rms + 1e-3 and h_p99 <= 3 * r_p99 + 1e-3
+        assert h_rms <= 3 * r_rms + 1e-3 and h_p99 <= 3 * r_p99 + 1e-3
         for n in names:
             if _bn_fed_bias(n):
                 assert (got[n] - gold[n]).abs().max().item() <= 2 * lr0 * (k + 1) + 1e-6, n
@@ -216,7 +212,7 @@ def test_trainer_matches_reference_training_loop(math):
         for kk in sd_now:
             if kk.endswith("num_batches_tracked"):
                 assert int(sd_now[kk]) == int(gold[kk]) == k + 1, kk
-            elif "running" in kk and (math == "h3" or k == 0):
+            elif "running" in kk:
                 e_h = (sd_now[kk].double() - sd64[kk]).abs().max().item()
                 e_r = (gold[kk].double() - sd64[kk]).abs().max().item()
                 assert e_h <= 3 * e_r + 1e-5 * sd64[kk].abs().max().item() + 1e-7, (kk, e_h, e_r)

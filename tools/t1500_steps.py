@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--steps", type=int, default=1500)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--layers", action="store_true", help="per-intermediate cumulative errors (w = 0)")
-    ap.add_argument("--override", default="", help="comma list of x0,d1,d2,emb,film2,u3: substitute the fp64 oracle's "
+    ap.add_argument("--override", default="", help="comma list of x0,d1,d2,emb,film2,u3,yO,eps: substitute the fp64 oracle's "
                                                      "value (rounded to fp32) there in every HIP forward (w = 0)")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
@@ -108,6 +108,13 @@ def main():
                     ws_.catU2.buf.view(n, H1, H1, 2 * nf)[..., :nf] = nhwc(I64o["film2"])
                 elif name == "d2":
                     ws_.catU1.buf.view(n, H2, H2, 4 * nf)[..., 2 * nf:] = nhwc(I64o["d2"])
+                elif name == "yO":      # out.0's pre-norm output; its GroupNorm statistics come from the conv epilogue
+                    ws_.yO.view(n, H, H, nf)[:] = nhwc(I64o["yO"])
+                    ws_.slab.zero_()
+                    yo = I64o["yO"].double()                      # exact per-(image, 128-pixel chunk) sums
+                    v = yo.permute(0, 2, 3, 1).reshape(n, H * H // 128, 128, nf)
+                    sl = torch.stack([v.sum(2), (v * v).sum(2)], 2).float().reshape(-1)
+                    ws_.slab[: sl.numel()] = sl.cuda()
                 elif name == "emb":
                     for k_, mname in (("cemb1", "contextembed1"), ("temb1", "timeembed1"), ("cemb2", "contextembed2"),
                                       ("temb2", "timeembed2")):
@@ -138,6 +145,8 @@ def main():
                 lay_h[key] = lay_h.get(key, 0) + (h_ - r)
                 lay_r[key] = lay_r.get(key, 0) + (I32[key].double().reshape(r.shape) - r)
                 lay_n[key] = lay_n.get(key, 0.0) + r.norm().item()
+        if "eps" in overrides:
+            e = I64o["eps"].float().cuda().reshape(B, 1, H, H)
         if cfg:
             eh = e[n:] + a.w * (e[:n] - e[n:])
             e32 = o32[1] + a.w * (o32[0] - o32[1])
@@ -165,6 +174,15 @@ def main():
         mx = np.abs(ref64).max()
         print(f"final x vs fp64: HIP (this loop) {np.abs(xh.cpu().numpy() - ref64).max() / mx:.3e}, reference fp32 "
               f"{np.abs(sfx[f'w{a.w:g}_x'] - ref64).max() / mx:.3e}")
+        dh = xh.cpu().numpy() - ref64
+        dr = sfx[f"w{a.w:g}_x"] - ref64
+        for name, d in (("HIP", dh), ("ref32", dr)):
+            k = np.unravel_index(np.abs(d).argmax(), d.shape)
+            print(f"  {name}: argmax {tuple(int(v) for v in k)} d {d[k]:.4g} x64 {ref64[k]:.6g} | L2 rel "
+                  f"{np.linalg.norm(d) / np.linalg.norm(ref64):.3e} | corr(HIP, ref32) "
+                  f"{float((dh * dr).sum() / np.linalg.norm(dh) / np.linalg.norm(dr)):.3f}")
+        np.savez_compressed(os.path.join(ROOT, "gpurun_out", f"t1500_final_{a.override or 'none'}.npz"),
+                            x_hip=xh.cpu().numpy(), x64=ref64, x32=sfx[f"w{a.w:g}_x"])
 
 
 if __name__ == "__main__":
