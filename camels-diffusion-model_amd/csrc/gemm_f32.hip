@@ -2373,6 +2373,10 @@ CDM_API int cdm_conv3x3_fwd_h3_ex(const float* x, int N, int H, int W, int Cin, 
 // the staggered wave order of the kernel-row weight gradient ($CDM_WGRAD_STAGGER=1; off: same-box A/B, 2 rounds,
 // C2 train step 52.11-52.42 -> 52.88-53.05 ms and C4 32.26-32.52 -> 33.38-33.61 ms with it on — the staging wave
 // then waits on the K step's loads it has just issued, profiles/r3_ab_wgrad_stagger.txt)
+static int wgrad_ks4() {
+    static const int v = [] { const char* e = getenv("CDM_WGRAD_KS4"); return e ? atoi(e) : 0; }();
+    return v;
+}
 static int wgrad_stagger() {
     static const int v = [] { const char* e = getenv("CDM_WGRAD_STAGGER"); return e ? atoi(e) : 0; }();
     return v;
@@ -2552,9 +2556,10 @@ CDM_API int cdm_conv3x3_wgrad_x16_ex(const float* g, int ldg, const float* y, in
         return (int)hipErrorInvalidValue;
     const int K = N * H * W, sp = effective_splits(K, splits);
     const bool ks2 = W % 32 == 0 && effective_splits(K, splits, 32) == sp;
-    // (64-pixel K steps for the one-term bf16 images measured 1.81x slower per launch than 32: 1284 vs 710 us on the
-    // C4 step's 128 -> 128 @64^2 weight gradients, profiles/r3_c4_ks4.txt — not used)
-    const bool ks4 = false;
+    // 64-pixel K steps ($CDM_WGRAD_KS4=1, bf16 activations only): with fp32 activations they measured 1.81x slower per
+    // launch than 32 (1284 vs 710 us, 22 VGPRs spilled, profiles/r3_c4_ks4.txt); the bf16 staging registers are half
+    // as wide (249 VGPRs, no spill)
+    const bool ks4 = wgrad_ks4() && W % 64 == 0 && effective_splits(K, splits, 64) == sp;
     if (!ks2 && effective_splits(K, splits, 16) != sp) return (int)hipErrorInvalidValue;
     const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
     const PreBnRelu px{{x_s, x_t}};
@@ -2566,9 +2571,16 @@ CDM_API int cdm_conv3x3_wgrad_x16_ex(const float* g, int ldg, const float* y, in
         using XT = decltype(xtag);
         const GT* gg = reinterpret_cast<const GT*>(g);
         const XT* xx = reinterpret_cast<const XT*>(x);
+        constexpr bool BF = !(std::is_same<GT, float>::value && std::is_same<XT, float>::value);
 #define CDM_WG(KS_, PRE_, PX_) launch_wgrad_row<KS_>(gg, ldg, Cout, xx, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, \
                                                      nterm, st, PRE_, PX_)
-#define CDM_WGK(PRE_, PX_) (ks4 ? CDM_WG(4, PRE_, PX_) : ks2 ? CDM_WG(2, PRE_, PX_) : CDM_WG(1, PRE_, PX_))
+        auto wgk = [&](auto pre_, auto px_) -> int {
+            if constexpr (BF) {
+                if (ks4) return CDM_WG(4, pre_, px_);
+            }
+            return ks2 ? CDM_WG(2, pre_, px_) : CDM_WG(1, pre_, px_);
+        };
+#define CDM_WGK(PRE_, PX_) wgk(PRE_, PX_)
         if (x_sums) {   // the producer's BN-backward sums ride along (x_sums[splits][5][Cin])
             if (y) return CDM_WGK(pre, pxs);
             return CDM_WGK(PreNone{}, pxs);

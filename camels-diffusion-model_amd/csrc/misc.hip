@@ -386,30 +386,33 @@ __global__ __launch_bounds__(256) void conv_cin1_dgrad_kernel(const float* g1, i
 // HBM once (+2/R halo rows) instead of 9 times through the caches.
 // gs / gt (optional, per (sample, channel) [N][C]): the input is relu(z gs + gt) of the pre-norm z (out.1's GroupNorm +
 // ReLU applied while staging, the fmaf of norm_apply_fwd: bit-identical to the applied tensor; padding stays zero)
+// HPM: halo pixels the LDS images hold, (R + 2) W rounded up to 64: 384 for W <= 64 (40 KiB of LDS, 4 blocks per CU;
+// the W-independent 768-pixel images took 80 KiB, 2 blocks per CU, half the loads in flight: 2.3 TB/s), 512 for W = 128,
+// 768 for W = 256
+template <int HPM>
 __global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* __restrict__ z, int ldz, int H, int W,
                                                                   int C, const float* __restrict__ w,
                                                                   const float* __restrict__ bias,
                                                                   float* __restrict__ out,
                                                                   const float* __restrict__ gs,
                                                                   const float* __restrict__ gt) {
-    constexpr int HPMAX = 512;                        // (R + 2) * W <= 256 + 2 * 128 for W <= 128; W = 256 -> 768
-    __shared__ float zt[3 * 256 * 17];                // [halo px][16 ch + 1 pad]
-    __shared__ float st[9 * 3 * 256];                 // [tap][halo px]
+    constexpr int KQ = (HPM + 255) / 256;             // halo pixels per thread in the tap reduction
+    __shared__ float zt[HPM * 17];                    // [halo px][16 ch + 1 pad]
+    __shared__ float st[9 * HPM];                     // [tap][halo px]
     const int R = 256 / W, HP = (R + 2) * W;
     // XCD-contiguous band order: the bands of an image run on one XCD, so the halo rows a band shares with its
     // neighbours come from that XCD's L2 (round-robin order fetched 1.68x the algorithmic bytes)
     const int L = xcd_logical_block();
     const int bands = H / R, n = L / bands, h0 = (L - n * bands) * R;
     const int tid = threadIdx.x;
-    (void)HPMAX;
-    float acc[3][9];
+    float acc[KQ][9];
 #pragma unroll
-    for (int k = 0; k < 3; ++k)
+    for (int k = 0; k < KQ; ++k)
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[k][t] = 0.f;
     // staging: piece i of this thread = (halo pixel q4>>2, channels 4(q4&3)..+3) of the current 16-channel slab;
     // the next slab's pieces are loaded into registers while this slab is reduced (one slab of latency hidden)
-    constexpr int PQ = 12;                            // (768 * 4) / 256
+    constexpr int PQ = HPM * 4 / 256;
     const float* src[PQ];
 #pragma unroll
     for (int i = 0; i < PQ; ++i) {
@@ -447,7 +450,7 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* _
         __syncthreads();
         if (c0 + 16 < C) gload(c0 + 16);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < KQ; ++k) {
             const int q = tid + k * 256;
             if (q < HP) {
 #pragma unroll
@@ -461,7 +464,7 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* _
         __syncthreads();
     }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < KQ; ++k) {
         const int q = tid + k * 256;
         if (q < HP) {
 #pragma unroll
@@ -731,37 +734,77 @@ __global__ __launch_bounds__(256) void embed_bwd_act_kernel(Mlp4 P) {
     }
 }
 
-// parameter grads (assign): dw2[j][i], db2[j], dw1[i][k], db1[i]; each a sequential fp64 sum over the rows, its loads
-// unrolled 8 deep (the row loop was one dependent global load per step: 166 us per C2 step, latency-bound)
+// parameter grads (assign): dw2[j][i], db2[j], dw1[i][k], db1[i]; each a sequential fp64 sum over the rows (the
+// product of two fp32 values is exact in fp64, so fma and multiply-add give the same bits).  dw2 (E x E outputs, the
+// bulk) in 64 x 64 tiles: the block stages 64 rows of dout and h through LDS and each thread carries 4 x 4 outputs, 16
+// independent fp64 chains (the per-output form waited on one global load per row: 40 us per C2 step, latency-bound);
+// blocks past the tiles take db2, dw1, db1 one output per thread.
+constexpr int EMB_T = 64;
+static __host__ __device__ inline int embed_tiles(int E) { return ((E + EMB_T - 1) / EMB_T) * ((E + EMB_T - 1) / EMB_T); }
 __global__ __launch_bounds__(256) void embed_bwd_param_kernel(Mlp4 P) {
     const MlpDesc& d = P.m[blockIdx.y];
     const int E = d.E, I = d.in_dim, rows = d.rows;
-    const long long n_w2 = (long long)E * E, n_all = n_w2 + E + (long long)E * I + E;
-    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n_all;
-         idx += (long long)gridDim.x * blockDim.x) {
-        double s = 0.0;
-        if (idx < n_w2) {
-            const int j = (int)(idx / E), i = (int)(idx - (long long)j * E);
-#pragma unroll 8
-            for (int b = 0; b < rows; ++b) s += (double)d.dout[(long long)b * E + j] * d.h[(long long)b * E + i];
-            d.dw2[idx] = (float)s;
-        } else if (idx < n_w2 + E) {
-            const int j = (int)(idx - n_w2);
-#pragma unroll 8
-            for (int b = 0; b < rows; ++b) s += d.dout[(long long)b * E + j];
-            d.db2[j] = (float)s;
-        } else if (idx < n_w2 + E + (long long)E * I) {
-            const long long q = idx - n_w2 - E;
-            const int i = (int)(q / I), k = (int)(q - (long long)i * I);
-#pragma unroll 8
-            for (int b = 0; b < rows; ++b) s += (double)d.dpre[(long long)b * E + i] * d.x[b * I + k];
-            d.dw1[q] = (float)s;
-        } else {
-            const int i = (int)(idx - n_w2 - E - (long long)E * I);
-#pragma unroll 8
-            for (int b = 0; b < rows; ++b) s += d.dpre[(long long)b * E + i];
-            d.db1[i] = (float)s;
+    const int nt = embed_tiles(E);
+    const int tid = threadIdx.x;
+    if ((int)blockIdx.x < nt) {
+        __shared__ __attribute__((aligned(16))) float ds_[EMB_T][EMB_T], hs_[EMB_T][EMB_T];
+        const int tpr = (E + EMB_T - 1) / EMB_T;
+        const int j0 = (blockIdx.x / tpr) * EMB_T, i0 = (blockIdx.x % tpr) * EMB_T;
+        const int tj = (tid >> 4) * 4, ti = (tid & 15) * 4;
+        double s[4][4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) s[a][c] = 0.0;
+        for (int b0 = 0; b0 < rows; b0 += EMB_T) {
+            const int nb = min(EMB_T, rows - b0);
+            for (int q = tid; q < EMB_T * EMB_T; q += 256) {
+                const int r = q / EMB_T, c = q - r * EMB_T;
+                const bool ok = r < nb;
+                ds_[r][c] = ok && j0 + c < E ? d.dout[(long long)(b0 + r) * E + j0 + c] : 0.f;
+                hs_[r][c] = ok && i0 + c < E ? d.h[(long long)(b0 + r) * E + i0 + c] : 0.f;
+            }
+            __syncthreads();
+            for (int r = 0; r < nb; ++r) {
+                const float4 dv = *reinterpret_cast<const float4*>(&ds_[r][tj]);
+                const float4 hv = *reinterpret_cast<const float4*>(&hs_[r][ti]);
+                const double dd[4] = {dv.x, dv.y, dv.z, dv.w}, hh[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) s[a][c] = fma(dd[a], hh[c], s[a][c]);
+            }
+            __syncthreads();
         }
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int j = j0 + tj + a, i = i0 + ti + c;
+                if (j < E && i < E) d.dw2[(long long)j * E + i] = (float)s[a][c];
+            }
+        return;
+    }
+    const long long n_rest = (long long)E + (long long)E * I + E;
+    const long long idx = (long long)(blockIdx.x - nt) * blockDim.x + tid;
+    if (idx >= n_rest) return;
+    double s = 0.0;
+    if (idx < E) {
+        const int j = (int)idx;
+#pragma unroll 8
+        for (int b = 0; b < rows; ++b) s += d.dout[(long long)b * E + j];
+        d.db2[j] = (float)s;
+    } else if (idx < E + (long long)E * I) {
+        const long long q = idx - E;
+        const int i = (int)(q / I), k = (int)(q - (long long)i * I);
+#pragma unroll 8
+        for (int b = 0; b < rows; ++b) s += (double)d.dpre[(long long)b * E + i] * d.x[b * I + k];
+        d.dw1[q] = (float)s;
+    } else {
+        const int i = (int)(idx - E - (long long)E * I);
+#pragma unroll 8
+        for (int b = 0; b < rows; ++b) s += d.dpre[(long long)b * E + i];
+        d.db1[i] = (float)s;
     }
 }
 
@@ -1073,15 +1116,24 @@ CDM_API int cdm_slab_sum_all(const double* part, int nparts, int R, int r0, int 
                        out, s_r, s_c, accumulate);
     return cdm_status();
 }
+static int launch_cout1_band(const float* z, int ldz, int N, int H, int W, int C, const float* w, const float* bias,
+                             float* out, const float* gs, const float* gt, hipStream_t st) {
+    const dim3 grid(N * (H / (256 / W)));
+    const int hp = (256 / W + 2) * W;           // halo pixels of a band
+    if (hp <= 384)
+        hipLaunchKernelGGL(conv_cout1_fwd_band_kernel<384>, grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
+    else if (hp <= 512)
+        hipLaunchKernelGGL(conv_cout1_fwd_band_kernel<512>, grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
+    else
+        hipLaunchKernelGGL(conv_cout1_fwd_band_kernel<768>, grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
+    return cdm_status();
+}
 CDM_API int cdm_conv3x3_cout1_fwd(const float* z, int ldz, int N, int H, int W, int C, const float* w, const float* bias,
                                   float* out, void* stream) {
     if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
     const long long P = (long long)N * H * W;
-    if (C % 16 == 0 && W <= 256 && 256 % W == 0 && H % (256 / W) == 0 && ldz % 4 == 0) {
-        hipLaunchKernelGGL(conv_cout1_fwd_band_kernel, dim3(N * (H / (256 / W))), dim3(256), 0, S(stream), z, ldz, H, W,
-                           C, w, bias, out, nullptr, nullptr);
-        return cdm_status();
-    }
+    if (C % 16 == 0 && W <= 256 && 256 % W == 0 && H % (256 / W) == 0 && ldz % 4 == 0)
+        return launch_cout1_band(z, ldz, N, H, W, C, w, bias, out, nullptr, nullptr, S(stream));
     hipLaunchKernelGGL(conv_cout1_fwd_kernel, dim3(nblocks(P, 256 / (C / 4), 8192)), dim3(256), 0, S(stream), z, ldz, N, H,
                        W, C, w, bias, out);
     return cdm_status();
@@ -1092,9 +1144,7 @@ CDM_API int cdm_conv3x3_cout1_fwd_gn(const float* y, int ldy, int N, int H, int 
                                      const float* gt, const float* w, const float* bias, float* out, void* stream) {
     if (C % 16 || C > 1024 || W > 256 || 256 % W || H % (256 / W) || ldy % 4 || !gs || !gt)
         return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(conv_cout1_fwd_band_kernel, dim3(N * (H / (256 / W))), dim3(256), 0, S(stream), y, ldy, H, W, C, w,
-                       bias, out, gs, gt);
-    return cdm_status();
+    return launch_cout1_band(y, ldy, N, H, W, C, w, bias, out, gs, gt, S(stream));
 }
 CDM_API int cdm_conv3x3_cin1_dgrad(const float* g1, int ldg, const float* y1, int ldy, const float* s, const float* t,
                                    const float* mean, const float* invstd, const float* A, const float* B,
@@ -1167,7 +1217,14 @@ CDM_API int cdm_embed_bwd(const Mlp4* P, void* stream) {
     for (int k = 0; k < 4; ++k) { rows = P->m[k].rows > rows ? P->m[k].rows : rows; if (P->m[k].E > 1024) return (int)hipErrorInvalidValue; }
     hipLaunchKernelGGL(embed_bwd_act_kernel, dim3(rows, 4), dim3(256), 0, S(stream), *P);
     int e = cdm_status(); if (e) return e;
-    hipLaunchKernelGGL(embed_bwd_param_kernel, dim3(256, 4), dim3(256), 0, S(stream), *P);
+    int nbx = 1;
+    for (int k = 0; k < 4; ++k) {
+        const MlpDesc& m = P->m[k];
+        const long long rest = 2LL * m.E + (long long)m.E * m.in_dim;
+        const int b = embed_tiles(m.E) + (int)((rest + 255) / 256);
+        nbx = b > nbx ? b : nbx;
+    }
+    hipLaunchKernelGGL(embed_bwd_param_kernel, dim3(nbx, 4), dim3(256), 0, S(stream), *P);
     return cdm_status();
 }
 CDM_API int cdm_perturb(const float* x, const float* noise, const int* t, const int* cur_i, long long nstride,

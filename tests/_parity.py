@@ -21,6 +21,18 @@ def _plain(v):
     return v
 
 
+def golden_schedule(T: int):
+    """(b_t, a_t, ab_t) fp32 CPU tensors the golden trajectories were made with (tests/golden/schedule.npz).
+
+    The schedule is computed on the host with torch's vectorised fp32 log / exp / sqrt, whose last bit depends on the
+    host's instruction set (tests/golden/add_schedules_r4.py): a trajectory test compares against a golden made on
+    another host only on that host's schedule, passed to the sampler as the reference's functional sampler takes it."""
+    import numpy as np
+    import torch
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "schedule.npz"))
+    return tuple(torch.from_numpy(fx[f"{k}_{T}"].copy()) for k in ("b_t", "a_t", "ab_t"))
+
+
 def record(name: str, **values):
     path = os.environ.get("CDM_PARITY_OUT")
     if not path:

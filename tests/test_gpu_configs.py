@@ -187,7 +187,7 @@ def test_c4_bf16_cfg_sampler_vs_reference_golden(w):
     m.load_state_dict(sd)
     m = m.cuda().eval()
     sfx = np.load(os.path.join(GOLD, "sampler_nf8.npz"))
-    d = cdm_amd.DDPM(m, int(sfx["T"]), "cuda", z_source="host")
+    d = cdm_amd.DDPM(m, int(sfx["T"]), "cuda", z_source="host", sched_tensors=_parity.golden_schedule(int(sfx["T"])))
     torch.manual_seed(500)                       # the reference's RNG state for this trajectory
     x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(sfx["params"]), w)
     # bar: 1.5x the error of the reference's own sampler under the same bf16 operand rounding (the CPU oracle, which
@@ -196,7 +196,7 @@ def test_c4_bf16_cfg_sampler_vs_reference_golden(w):
     with _bf16_operands():
         torch.manual_seed(500)
         xe, inte = R.sample_ddpm(R.make_model_fn(R.clone_sd(sd), n_feat=8, n_cfeat=6, height=64), 2, 64,
-                                 torch.from_numpy(sfx["params"]), w, T, R.make_schedule(T), 6)
+                                 torch.from_numpy(sfx["params"]), w, T, _parity.golden_schedule(T), 6)
     gx, gi = torch.from_numpy(sfx[f"sample_w{w:g}"]), torch.from_numpy(sfx[f"sample_w{w:g}_inter"])
     e_hip, e_emu = _rel(x, gx), _rel(xe, gx)
     ei_hip, ei_emu = _rel(torch.from_numpy(inter), gi), _rel(inte, gi)
@@ -271,14 +271,14 @@ def test_c4_bf16_cfg_T1500_vs_emulated_oracle(w):
     m = cdm_amd.ContextUnet(1, 8, 6, 64, conv_math="bf16")
     m.load_state_dict(sd)
     m = m.cuda().eval()
-    d = cdm_amd.DDPM(m, T, "cuda", z_source="host")
+    d = cdm_amd.DDPM(m, T, "cuda", z_source="host", sched_tensors=_parity.golden_schedule(T))
     seed = int(sfx[f"w{w:g}_seed"])
     torch.manual_seed(seed)
     x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(sfx["params"]), w)
     with _bf16_operands():
         torch.manual_seed(seed)
         xe, inte = R.sample_ddpm(R.make_model_fn(R.clone_sd(sd), n_feat=8, n_cfeat=6, height=64), 2, 64,
-                                 torch.from_numpy(sfx["params"]), w, T, R.make_schedule(T), 6)
+                                 torch.from_numpy(sfx["params"]), w, T, _parity.golden_schedule(T), 6)
     keep = sfx["snap_keep"]
 
     def errs(final, snaps):

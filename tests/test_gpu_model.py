@@ -315,7 +315,8 @@ def test_bn_sums_in_consumer_wgrad_nf128(math):
     import cdm_amd.model as M
     eng = M.get_engine(nf, 6, 64, torch.device("cuda", torch.cuda.current_device()), math)
     res = []
-    sums0 = eng.fuse_bn_sums
+    sums0, act0 = eng.fuse_bn_sums, eng.act16
+    eng.act16 = False        # bf16 activations need the fused sums (the separate pass reads fp32 y / g): fp32 both ways
     try:
         for on in (True, False):
             eng.fuse_bn_sums = on
@@ -329,7 +330,7 @@ def test_bn_sums_in_consumer_wgrad_nf128(math):
             res.append((pred.detach().cpu(), {k: p.grad.detach().double().cpu() for k, p in m.named_parameters()},
                         {k: v.detach().cpu() for k, v in m.state_dict().items() if "running" in k}))
     finally:
-        eng.fuse_bn_sums = sums0
+        eng.fuse_bn_sums, eng.act16 = sums0, act0
         M._WS.clear()
     assert torch.equal(res[0][0], res[1][0])
     for k in res[1][2]:

@@ -43,7 +43,7 @@ def test_sample_ddpm_cfg_matches_reference(w):
     import cdm_amd
     sfx = np.load(os.path.join(GOLD, "sampler_nf8.npz"))
     T = int(sfx["T"])
-    d = cdm_amd.DDPM(_model(), T, "cuda", z_source="host")
+    d = cdm_amd.DDPM(_model(), T, "cuda", z_source="host", sched_tensors=_parity.golden_schedule(T))
     torch.manual_seed(500)
     x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(sfx["params"]), w)
     assert _rel(x, sfx[f"sample_w{w:g}"]) < 1e-3
@@ -55,7 +55,7 @@ def test_sample_random_params_and_from_noise():
     import cdm_amd
     sfx = np.load(os.path.join(GOLD, "sampler_nf8.npz"))
     T = int(sfx["T"])
-    d = cdm_amd.DDPM(_model(), T, "cuda", z_source="host")
+    d = cdm_amd.DDPM(_model(), T, "cuda", z_source="host", sched_tensors=_parity.golden_schedule(T))
     torch.manual_seed(501)
     x, _ = d.sample_ddpm(2, 64, None, None, 0.0)
     assert _rel(x, sfx["sample_noparams"]) < 1e-3
@@ -89,6 +89,52 @@ def test_perturb_and_denoise_bit_exact():
     assert torch.equal(cdm_amd.denoise_add_noise(x.cuda(), 1, eps.cuda(), 0, sched).cpu(), ref)
 
 
+def test_host_schedule_vs_golden():
+    """The schedule (code/train_diffusion_condition.py:96-99) the HIP Schedule builds on THIS host with the reference's
+    fp32 torch expressions vs the one the golden trajectories were made with: equal up to the last bit of the
+    vectorised log / exp / sqrt of the host's instruction set, which ab_t's cumulative sum of logs carries along
+    (recorded: the count of entries that differ and the largest difference in ulp; bar 64 ulp, measured 8.2 at T = 1500
+    on the GPU box).  The golden-trajectory tests run on the golden's schedule (_parity.golden_schedule)."""
+    import cdm_amd
+    rec = {}
+    for T in (10, 400, 1500):
+        g = _parity.golden_schedule(T)
+        s = cdm_amd.Schedule(T, "cpu")
+        for name, mine, gold in zip(("b_t", "a_t", "ab_t"), s.tensors(), g):
+            diff = mine != gold
+            rec[f"{name}_{T}"] = int(diff.sum())
+            if diff.any():
+                ulp = (mine[diff].double() - gold[diff].double()).abs() / torch.finfo(torch.float32).eps \
+                    / gold[diff].double().abs()
+                rec[f"{name}_{T}_max_ulp"] = ulp.max().item()
+                assert ulp.max().item() <= 64, (name, T, ulp.max().item())
+    _parity.record("host_schedule_vs_golden", **rec)
+    print("schedule entries that differ from the golden's:", rec)
+
+
+def test_host_rng_vs_golden():
+    """torch's CPU RNG draws of the T = 1500 golden's order (x_T, z, shortcut; tests/golden/add_host_rng_r4.py) on THIS
+    host vs the container that made the goldens: the uniform draws (the shortcut) are host-independent, the normal
+    ones (Box-Muller through vectorised log / sin / cos) may differ in the last bit.  Recorded, bar 4 ulp of the
+    largest |draw|: a CPU-RNG-replay trajectory test on another host replays z up to those bits."""
+    sys_path = os.path.join(GOLD, "add_host_rng_r4.py")
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("add_host_rng_r4", sys_path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    fx = np.load(os.path.join(GOLD, "host_rng.npz"))
+    mine = mod.draws()
+    rec = {"cpu_capability": torch.backends.cpu.get_cpu_capability(), "golden_cpu_capability": str(fx["cpu_capability"])}
+    for k, v in mine.items():
+        d = np.abs(v.astype(np.float64) - fx[k])
+        rec[k + "_ndiff"] = int((d > 0).sum())
+        rec[k + "_max_ulp"] = float(d.max() / (np.finfo(np.float32).eps * np.abs(fx[k]).max()))
+        assert rec[k + "_max_ulp"] <= 4, (k, rec)
+    assert rec["sc_w_ndiff"] == 0 and rec["sc_b_ndiff"] == 0
+    _parity.record("host_rng_vs_golden", **rec)
+    print("host CPU-RNG draws vs the golden's:", rec)
+
+
 def test_graph_replay_equals_eager():
     import cdm_amd
     m = _model()
@@ -108,51 +154,75 @@ def test_graph_replay_equals_eager():
 
 
 # ---------------------------------------------------------------------------------------------------------------
-# T = 1500, the benchmarked trajectory length (reference golden: tests/golden/make_golden_r2.py)
+# T = 1500, the benchmarked trajectory length (reference golden: tests/golden/make_golden_r2.py), and n_feat = 128
 # ---------------------------------------------------------------------------------------------------------------
+# The bar of both trajectory tests: HIP's deviation from the reference's fp64 re-run, relative to max|x|, at the final x
+# and at every stored snapshot, within 1.5x the reference's own fp32 deviation, no floor.  The reference's fp32 error
+# along these trajectories is chaotic: the same fp32 program on the GPU box's host (the CPU oracle, torch's CPU kernels
+# there, the golden's schedule and RNG draws, which are bit-identical there: test_host_schedule_vs_golden /
+# test_host_rng_vs_golden) ends 1.01e-5 of max|x| away from fp64 at T = 1500, w = 0 — 2.9x what the golden's host got
+# (3.5e-6) — while each step's network error is the same size (tools/t1500_steps.py: per-step local error HIP 1.96e-7,
+# reference 2.40e-7 of |eps|).  So the reference's fp32 deviation is taken as the larger of the two hosts' runs: the
+# golden's, and the CPU oracle's on this host (computed here, the test's checker).
+_REF32 = {}
+
+
+def _ref32_on_host(key, sd, nf, params, w, T, seed):
+    """The reference's fp32 sampler (oracle/ref_cpu.py, torch CPU fp32) on this host: final x and all snapshots."""
+    if key not in _REF32:
+        torch.set_num_threads(min(16, max(1, len(os.sched_getaffinity(0)))))
+        fn = R.make_model_fn(R.clone_sd(sd), n_feat=nf, n_cfeat=6, height=64)
+        torch.manual_seed(seed)
+        with torch.no_grad():
+            x, inter = R.sample_ddpm(fn, 2, 64, params, w, T, _parity.golden_schedule(T), 6)
+        _REF32[key] = (x.numpy(), np.asarray(inter))
+    return _REF32[key]
+
+
+def _trajectory_check(name, sfx, x, inter, host, w, **rec):
+    """final / per-snapshot deviations from fp64 of HIP, the golden's fp32 reference and this host's; 1.5x bar"""
+    ref64 = sfx[f"w{w:g}_x_fp64"]
+    mx = np.abs(ref64).max()
+    hx, hinter = host
+
+    def dev(a, r):
+        return float(np.abs(np.asarray(a, np.float64) - r).max() / np.abs(r).max())
+    rows = [("final", dev(x, ref64), dev(sfx[f"w{w:g}_x"], ref64), dev(hx, ref64))]
+    for j, sl in enumerate(sfx["snap_keep"]):
+        r = sfx[f"w{w:g}_inter_fp64"][j]
+        rows.append((int(sl), dev(inter[sl], r), dev(sfx[f"w{w:g}_inter"][j], r), dev(hinter[sl], r)))
+    print(f"{name} w={w:g} {rec}: max|x| {mx:.3g}; deviation from fp64 HIP / reference fp32 (golden host, this host): "
+          + " ".join(f"{a}:{b:.2e}/{c:.2e},{d:.2e}" for a, b, c, d in rows))
+    _parity.record(name, w=w, max_abs_x=float(mx), final_err=rows[0][1], final_err_ref32=rows[0][2],
+                   final_err_ref32_this_host=rows[0][3],
+                   snapshots=[{"slot": a, "err": b, "err_ref32": c, "err_ref32_this_host": d} for a, b, c, d in rows[1:]],
+                   **rec)
+    for a, b, c, d in rows:
+        assert b <= 1.5 * max(c, d), f"{name} w={w:g} at {a}: HIP {b:.3e} vs reference {c:.3e} / {d:.3e}"
+
+
 @pytest.mark.parametrize("w,math", [(0.0, "h3"), (0.0, "fp32"), (3.0, "h3")])
 def test_sample_T1500_matches_reference(w, math):
-    """sample_ddpm at T=1500 (code/train_diffusion_condition.py:281-335), CPU-RNG replay (z_source="host").
-
-    Tolerance relative to max|x| (errors scale with |x|, which reaches ~1e4 with these untrained
-    weights), anchored on the reference's own fp32 deviation from the same trajectory run in fp64 (3.5e-6 (w=0) /
-    3.9e-6 (w=3) of max|x| at the end): for the final x and every stored snapshot, the HIP deviation from fp64 must
-    stay within 3x the reference's fp32 deviation at that snapshot plus a floor of 2e-6 max|x| (the reference's
-    deviation after ~1/3 of the trajectory; snapshots near x_T have deviations of 1e-7, where a fixed multiple of
-    the reference's error would be a bar below one fp32 rounding of the 1e4-sized values).  Measured (GPU box,
-    profiles/r3_parity.json): HIP 1.06e-5 / 9.8e-6 of max|x| at the end, 2.5-3.0x the reference's (identical under
-    h3 and the fp32 MFMA: the residual is not the 3x3-conv arithmetic)."""
+    """sample_ddpm at T=1500 (code/train_diffusion_condition.py:281-335), CPU-RNG replay (z_source="host") of the
+    reference's run, n_feat = 8 (tests/golden/make_golden_r2.py).  Errors scale with |x|, which reaches ~1e4 with
+    these untrained weights.  Bar: _trajectory_check (1.5x the reference's own fp32 deviation from its fp64
+    re-run at the final x and at each of the 13 stored snapshots, no floor)."""
     import cdm_amd
     sfx = np.load(os.path.join(GOLD, "sampler_T1500_nf8.npz"))
     T = int(sfx["T"])
-    m = _model()
-    if math != m.conv_math:
-        m = cdm_amd.ContextUnet(1, 8, 6, 64, conv_math=math)
-        fx = np.load(os.path.join(GOLD, "model_nf8.npz"))
-        m.load_state_dict({k[3:]: torch.from_numpy(fx[k].copy()) for k in fx.files if k.startswith("sd.")})
-        m = m.cuda().eval()
-    d = cdm_amd.DDPM(m, T, "cuda", z_source="host")
-    torch.manual_seed(int(sfx[f"w{w:g}_seed"]))
-    x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(sfx["params"]), w)
-    x = x.cpu().numpy()
+    fx = np.load(os.path.join(GOLD, "model_nf8.npz"))
+    sd = {k[3:]: torch.from_numpy(fx[k].copy()) for k in fx.files if k.startswith("sd.")}
+    m = cdm_amd.ContextUnet(1, 8, 6, 64, conv_math=math)
+    m.load_state_dict(sd)
+    m = m.cuda().eval()
+    params = torch.from_numpy(sfx["params"])
+    seed = int(sfx[f"w{w:g}_seed"])
+    d = cdm_amd.DDPM(m, T, "cuda", z_source="host", sched_tensors=_parity.golden_schedule(T))
+    torch.manual_seed(seed)
+    x, inter = d.sample_ddpm(2, 64, None, params, w)
     assert inter.shape[0] == 82
-    ref64, ref32 = sfx[f"w{w:g}_x_fp64"], sfx[f"w{w:g}_x"]
-    mx = np.abs(ref64).max()
-    e_hip, e_ref = np.abs(x - ref64).max() / mx, np.abs(ref32 - ref64).max() / mx
-    print(f"T=1500 w={w:g} [{math}]: max|x| {mx:.3g}; vs fp64: HIP {e_hip:.2e}, reference fp32 {e_ref:.2e}; "
-          f"HIP vs reference fp32 {np.abs(x - ref32).max() / mx:.2e}")
-    keep = sfx["snap_keep"]
-    snaps = []
-    for j, s in enumerate(keep):
-        r = sfx[f"w{w:g}_inter_fp64"][j]
-        rm = np.abs(r).max()
-        snaps.append((int(s), float(np.abs(inter[s] - r).max() / rm), float(np.abs(sfx[f"w{w:g}_inter"][j] - r).max() / rm)))
-    _parity.record("sample_T1500", w=w, conv_math=math, max_abs_x=float(mx), final_err=float(e_hip),
-                   final_err_ref32=float(e_ref), snapshots=[{"slot": a, "err": b, "err_ref32": c} for a, b, c in snaps])
-    floor = 2e-6
-    assert e_hip <= 3 * e_ref + floor, (e_hip, e_ref)
-    for s, e, er in snaps:
-        assert e <= 3 * er + floor, f"snapshot {s}: {e:.3e} vs reference {er:.3e}"
+    host = _ref32_on_host(("T1500", w), sd, 8, params, w, T, seed)
+    _trajectory_check("sample_T1500", sfx, x.cpu().numpy(), inter, host, w, conv_math=math)
 
 
 @pytest.mark.parametrize("w", [0.0, 3.0])
@@ -161,33 +231,21 @@ def test_sample_nf128_matches_reference(w):
     init, the reference's own weights for torch.manual_seed(0)), n = 2, w = 0 and the batched 2n CFG forward at w = 3,
     T = 400, CPU-RNG replay, vs the reference's trajectory re-run in fp64 (tests/golden/make_golden_r4.py).  Every layer
     runs the bench's kernels: the LDS-halo eval convs with BatchNorm folded, out.1's GroupNorm in out.3's staging, the
-    16-bit ConvT.  Bar: final x and every stored snapshot within 3x the reference's own fp32 deviation from fp64 at that
-    snapshot, plus one fp32 rounding of max|x| (2^-23)."""
+    16-bit ConvT.  Bar: _trajectory_check (1.5x the reference's own fp32 deviation, no floor)."""
     import cdm_amd
     sfx = np.load(os.path.join(GOLD, "sampler_T400_nf128.npz"))
     T, nf = int(sfx["T"]), int(sfx["n_feat"])
     torch.manual_seed(int(sfx["init_seed"]))
-    m = cdm_amd.ContextUnet(1, nf, 6, 64).cuda().eval()
-    d = cdm_amd.DDPM(m, T, "cuda", z_source="host")
-    torch.manual_seed(int(sfx[f"w{w:g}_seed"]))
-    x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(sfx["params"]), w)
-    x = x.cpu().numpy()
-    ref64, ref32 = sfx[f"w{w:g}_x_fp64"], sfx[f"w{w:g}_x"]
-    mx = np.abs(ref64).max()
-    e_hip, e_ref = np.abs(x - ref64).max() / mx, np.abs(ref32 - ref64).max() / mx
-    floor = 2.0 ** -23
-    snaps = []
-    for j, sl in enumerate(sfx["snap_keep"]):
-        r = sfx[f"w{w:g}_inter_fp64"][j]
-        rm = np.abs(r).max()
-        snaps.append((int(sl), float(np.abs(inter[sl] - r).max() / rm), float(np.abs(sfx[f"w{w:g}_inter"][j] - r).max() / rm)))
-    print(f"nf=128 T={T} w={w:g} [{m.conv_math}]: vs fp64 HIP {e_hip:.2e}, reference fp32 {e_ref:.2e}; snapshots "
-          + " ".join(f"{a}:{b:.1e}/{c:.1e}" for a, b, c in snaps))
-    _parity.record("sample_nf128_T400", w=w, conv_math=m.conv_math, max_abs_x=float(mx), final_err=float(e_hip),
-                   final_err_ref32=float(e_ref), snapshots=[{"slot": a, "err": b, "err_ref32": c} for a, b, c in snaps])
-    assert e_hip <= 3 * e_ref + floor, (e_hip, e_ref)
-    for sl, e, er in snaps:
-        assert e <= 3 * er + floor, f"snapshot {sl}: {e:.3e} vs reference {er:.3e}"
+    m = cdm_amd.ContextUnet(1, nf, 6, 64)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.cuda().eval()
+    params = torch.from_numpy(sfx["params"])
+    seed = int(sfx[f"w{w:g}_seed"])
+    d = cdm_amd.DDPM(m, T, "cuda", z_source="host", sched_tensors=_parity.golden_schedule(T))
+    torch.manual_seed(seed)
+    x, inter = d.sample_ddpm(2, 64, None, params, w)
+    host = _ref32_on_host(("nf128", w), sd, nf, params, w, T, seed)
+    _trajectory_check("sample_nf128_T400", sfx, x.cpu().numpy(), inter, host, w, conv_math=m.conv_math)
 
 
 def test_device_z_fresh_per_call_and_seedable():

@@ -11,4 +11,5 @@ export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o train -- \
     python3 $R/tools/train_profile.py --steps 10 --warmup 3 "$@" > $OUT/train.log 2> $OUT/train.err
 python3 $R/tools/kstep.py $OUT/train_kernel_trace.csv 8 > $OUT/breakdown.txt
+python3 $R/tools/kseq.py $OUT/train_kernel_trace.csv > $OUT/sequence.txt
 rm -f $OUT/train_kernel_trace.csv
