@@ -847,6 +847,9 @@ struct PreBnBwd {
     static constexpr int kind = 1;
     const float* y; int ldy;   // pre-norm activations [pix][C]
     const float* p[7];         // per channel: scale s, shift t, mean, invstd, A, B, Cc
+    void* dyo = nullptr;       // LDS-halo dgrad only (optional): the dy it computes is also stored here, element type and
+                               // row stride those of g, each element once (the block's own rows, column block 0), for
+                               // the layer's weight gradient to read instead of recomputing it from g and y
 };
 // PreBnRelu: the operand is z = relu(y s + t) of a Conv -> BatchNorm -> ReLU layer (train mode), computed while
 // staging from the layer's pre-norm output y: z is never written (the apply kernel's 537 MB write + read at 64^2).
@@ -1045,6 +1048,19 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
                     for (int e = 0; e < 4; ++e)
                         xv[e] = bn_bwd_elem(xv[e], f4get(yv, e), cf[0][e], cf[1][e], cf[2][e], cf[3][e],
                                             cf[4][e], cf[5][e], cf[6][e]);
+                    if (pre.dyo != nullptr && blockIdx.y == 0) {   // block-uniform
+                        // piece j's halo pixel (hr, hc) is one of the tile's own output pixels: rows 1..ROWS, columns
+                        // 1..WT of the halo (always inside the image); hxo[j] addresses it in g, same layout as dyo
+                        const int q = tid + j * HTHREADS, hp = q >> 2, hr = hp / HC, hc = hp - hr * HC;
+                        if (q < HPX * 4 && hr >= 1 && hr <= ROWS && hc >= 1 && hc <= WT) {
+                            char* o = reinterpret_cast<char*>(pre.dyo) + hxo[j] + (size_t)cc * 16 * XSZ;
+                            if constexpr (std::is_same<XT, float>::value)
+                                *reinterpret_cast<float4*>(o) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+                            else
+                                *reinterpret_cast<bf16x4*>(o) = bf16x4{(__bf16)xv[0], (__bf16)xv[1], (__bf16)xv[2],
+                                                                       (__bf16)xv[3]};
+                        }
+                    }
                 } else if constexpr (PRE::kind == 2) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) xv[e] = bn_relu_elem(xv[e], cf[0][e], cf[1][e]);
@@ -1679,6 +1695,9 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
         if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + ielems * 2) = bf16x4{m[0], m[1], m[2], m[3]};
         if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + ielems * 4) = bf16x4{l[0], l[1], l[2], l[3]};
     };
+    // one-term bf16 operands without a staging transform are copied as they arrive (no convert round trip)
+    constexpr bool RAWG = NT == 1 && !PRE::on && std::is_same<GT, __bf16>::value;
+    constexpr bool RAWX = NT == 1 && PX::kind == 0 && std::is_same<XT, __bf16>::value;
     auto sstore = [&](__bf16* buf) {
         char* a = reinterpret_cast<char*>(buf);
         char* b = a + NS * IA * 2;
@@ -1693,20 +1712,30 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
                     gv[e] = bn_bwd_elem(gv[e], yv[e], cf[0][e], cf[1][e], cf[2][e], cf[3][e], cf[4][e], cf[5][e],
                                         cf[6][e]);
                 put(a, sr + 16 * k, make_float4(gv[0], gv[1], gv[2], gv[3]), sa, IA);
+            } else if constexpr (RAWG) {   // bf16 dy (stored by the dgrad) into the one-term image: a plain copy
+                *reinterpret_cast<uint2*>(a + trswz(sr + 16 * k, c4 >> 3) + (c4 & 7) * 2) = ra[k];
             } else {
                 put(a, sr + 16 * k, Act<GT>::to4(ra[k]), sa, IA);
             }
-            const float4 xk = Act<XT>::to4(rb[k]);
-            if constexpr (SUMS) {
-                if (sum_step && (k > 0 || sr >= 1)) xsum(xk, Act<XT>::to4(gr[k]));
+            if constexpr (RAWX) {
+                *reinterpret_cast<uint2*>(b + trswz(sr + 16 * k, c4 >> 3) + (c4 & 7) * 2) = rb[k];
+            } else {
+                const float4 xk = Act<XT>::to4(rb[k]);
+                if constexpr (SUMS) {
+                    if (sum_step && (k > 0 || sr >= 1)) xsum(xk, Act<XT>::to4(gr[k]));
+                }
+                put(b, sr + 16 * k, xpre(xk, vb[k]), sb, IB);
             }
-            put(b, sr + 16 * k, xpre(xk, vb[k]), sb, IB);
         }
-        const float4 x1 = Act<XT>::to4(rb1);
-        if constexpr (SUMS) {
-            if (sum_step && tid < 32) xsum(x1, Act<XT>::to4(gr1));
+        if constexpr (RAWX) {
+            if (tid < 64) *reinterpret_cast<uint2*>(b + trswz(RA + sr, c4 >> 3) + (c4 & 7) * 2) = rb1;
+        } else {
+            const float4 x1 = Act<XT>::to4(rb1);
+            if constexpr (SUMS) {
+                if (sum_step && tid < 32) xsum(x1, Act<XT>::to4(gr1));
+            }
+            if (tid < 64) put(b, RA + sr, xpre(x1, vb1), sb, IB);
         }
-        if (tid < 64) put(b, RA + sr, xpre(x1, vb1), sb, IB);
     };
     // transposed-read addresses (see the per-tap kernel); tap t reads X rows shifted by t
     const int g = (lane >> 4) & 3, q = (lane >> 2) & 3, pq = lane & 3;
@@ -2289,16 +2318,19 @@ static bool x16_amax_ok(int nterm, const void* a, const void* b) { return nterm 
 // input dy = bn_bwd_elem(g, y, coefficients) is computed per staged element (dy never materialised).  C = BN
 // channels (the dgrad's input channels), Cout = the dgrad's output channels.  W == H in {32, 64, 128}, C % 16 == 0,
 // C <= 256; wx = cdm_split_f16x2 of the kc = 16 packed dgrad weights; max|dy| <= *amax_dy (cdm_bn_bwd_amax_bound).
-CDM_API int cdm_conv3x3_dgrad_x16_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
-                                        const float* t, const float* mean, const float* invstd, const float* A,
-                                        const float* B, const float* Cc, int N, int H, int W, int C, const void* wx,
-                                        const float* amax_dy, const float* amax_w, float* out, int ldo, int Cout,
-                                        int flags, float* amax_out, int nterm, int dt, void* stream) {
+// dy_out (optional): the dy computed in the staging is also stored there ([pix][C] at g's row stride ldg, g's element
+// type), for the layer's weight gradient (cdm_conv3x3_wgrad_x16_ex with dy = dy_out and no BN coefficients).
+CDM_API int cdm_conv3x3_dgrad_x16_bnbwd_dy(const float* g, int ldg, const float* y, int ldy, const float* s,
+                                           const float* t, const float* mean, const float* invstd, const float* A,
+                                           const float* B, const float* Cc, int N, int H, int W, int C, const void* wx,
+                                           const float* amax_dy, const float* amax_w, float* out, int ldo, int Cout,
+                                           int flags, float* amax_out, void* dy_out, int nterm, int dt, void* stream) {
     if (!x16_ok(nterm) || W != H || !halo_width_ok(W, nterm) || W > 128 || C % 16 || C > 256 || ldg % 4 || ldy % 4 ||
         (H * W) % HBM_ || !x16_amax_ok(nterm, amax_dy, amax_w) || (dt && nterm != 1))
         return (int)hipErrorInvalidValue;
     const int M = N * H * W;
-    const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
+    PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
+    pre.dyo = dy_out;
     const __bf16* b = reinterpret_cast<const __bf16*>(wx);
     // dt bit 0: g and y are bf16, bit 1: the output (the producer's g) is stored as bf16
     auto run = [&](auto xtag, auto otag) {
@@ -2315,6 +2347,14 @@ CDM_API int cdm_conv3x3_dgrad_x16_bnbwd(const float* g, int ldg, const float* y,
         case 3: return run(__bf16{}, __bf16{});
         default: return run(float{}, float{});
     }
+}
+CDM_API int cdm_conv3x3_dgrad_x16_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
+                                        const float* t, const float* mean, const float* invstd, const float* A,
+                                        const float* B, const float* Cc, int N, int H, int W, int C, const void* wx,
+                                        const float* amax_dy, const float* amax_w, float* out, int ldo, int Cout,
+                                        int flags, float* amax_out, int nterm, int dt, void* stream) {
+    return cdm_conv3x3_dgrad_x16_bnbwd_dy(g, ldg, y, ldy, s, t, mean, invstd, A, B, Cc, N, H, W, C, wx, amax_dy, amax_w,
+                                          out, ldo, Cout, flags, amax_out, nullptr, nterm, dt, stream);
 }
 CDM_API int cdm_conv3x3_dgrad_h3_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s,
                                        const float* t, const float* mean, const float* invstd, const float* A,
@@ -2374,7 +2414,7 @@ CDM_API int cdm_conv3x3_fwd_h3_ex(const float* x, int N, int H, int W, int Cin, 
 // C2 train step 52.11-52.42 -> 52.88-53.05 ms and C4 32.26-32.52 -> 33.38-33.61 ms with it on — the staging wave
 // then waits on the K step's loads it has just issued, profiles/r3_ab_wgrad_stagger.txt)
 static int wgrad_ks4() {
-    static const int v = [] { const char* e = getenv("CDM_WGRAD_KS4"); return e ? atoi(e) : 0; }();
+    static const int v = [] { const char* e = getenv("CDM_WGRAD_KS4"); return e ? atoi(e) : 1; }();
     return v;
 }
 static int wgrad_stagger() {
@@ -2556,9 +2596,9 @@ CDM_API int cdm_conv3x3_wgrad_x16_ex(const float* g, int ldg, const float* y, in
         return (int)hipErrorInvalidValue;
     const int K = N * H * W, sp = effective_splits(K, splits);
     const bool ks2 = W % 32 == 0 && effective_splits(K, splits, 32) == sp;
-    // 64-pixel K steps ($CDM_WGRAD_KS4=1, bf16 activations only): with fp32 activations they measured 1.81x slower per
-    // launch than 32 (1284 vs 710 us, 22 VGPRs spilled, profiles/r3_c4_ks4.txt); the bf16 staging registers are half
-    // as wide (249 VGPRs, no spill)
+    // 64-pixel K steps for bf16 activations ($CDM_WGRAD_KS4=0: 32): with fp32 activations they measured 1.81x slower
+    // per launch than 32 (1284 vs 710 us, 22 VGPRs spilled, profiles/r3_c4_ks4.txt); the bf16 staging registers are
+    // half as wide (249 VGPRs, no spill): C4 29.64-29.89 -> 29.31-29.44 ms per step (profiles/r4_ab_dy_store_ks4.txt)
     const bool ks4 = wgrad_ks4() && W % 64 == 0 && effective_splits(K, splits, 64) == sp;
     if (!ks2 && effective_splits(K, splits, 16) != sp) return (int)hipErrorInvalidValue;
     const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};

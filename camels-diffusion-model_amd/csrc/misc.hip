@@ -758,11 +758,20 @@ __global__ __launch_bounds__(256) void embed_bwd_param_kernel(Mlp4 P) {
             for (int c = 0; c < 4; ++c) s[a][c] = 0.0;
         for (int b0 = 0; b0 < rows; b0 += EMB_T) {
             const int nb = min(EMB_T, rows - b0);
-            for (int q = tid; q < EMB_T * EMB_T; q += 256) {
-                const int r = q / EMB_T, c = q - r * EMB_T;
+            // the chunk's 2 x 16 loads per thread issued together (then stored): one memory latency per chunk
+            float dv_[EMB_T * EMB_T / 256], hv_[EMB_T * EMB_T / 256];
+#pragma unroll
+            for (int u = 0; u < EMB_T * EMB_T / 256; ++u) {
+                const int q = tid + u * 256, r = q / EMB_T, c = q - r * EMB_T;
                 const bool ok = r < nb;
-                ds_[r][c] = ok && j0 + c < E ? d.dout[(long long)(b0 + r) * E + j0 + c] : 0.f;
-                hs_[r][c] = ok && i0 + c < E ? d.h[(long long)(b0 + r) * E + i0 + c] : 0.f;
+                dv_[u] = ok && j0 + c < E ? d.dout[(long long)(b0 + r) * E + j0 + c] : 0.f;
+                hv_[u] = ok && i0 + c < E ? d.h[(long long)(b0 + r) * E + i0 + c] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < EMB_T * EMB_T / 256; ++u) {
+                const int q = tid + u * 256, r = q / EMB_T, c = q - r * EMB_T;
+                ds_[r][c] = dv_[u];
+                hs_[r][c] = hv_[u];
             }
             __syncthreads();
             for (int r = 0; r < nb; ++r) {
@@ -791,18 +800,18 @@ __global__ __launch_bounds__(256) void embed_bwd_param_kernel(Mlp4 P) {
     double s = 0.0;
     if (idx < E) {
         const int j = (int)idx;
-#pragma unroll 8
+#pragma unroll 32
         for (int b = 0; b < rows; ++b) s += d.dout[(long long)b * E + j];
         d.db2[j] = (float)s;
     } else if (idx < E + (long long)E * I) {
         const long long q = idx - E;
         const int i = (int)(q / I), k = (int)(q - (long long)i * I);
-#pragma unroll 8
+#pragma unroll 32
         for (int b = 0; b < rows; ++b) s += (double)d.dpre[(long long)b * E + i] * d.x[b * I + k];
         d.dw1[q] = (float)s;
     } else {
         const int i = (int)(idx - E - (long long)E * I);
-#pragma unroll 8
+#pragma unroll 32
         for (int b = 0; b < rows; ++b) s += d.dpre[(long long)b * E + i];
         d.db1[i] = (float)s;
     }

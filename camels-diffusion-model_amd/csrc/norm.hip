@@ -248,6 +248,23 @@ __global__ void bn_eval_coeffs_kernel(int C, const float* gamma, const float* be
     mean[c] = rmean[c]; invstd[c] = is; scale[c] = sc; shift[c] = beta[c] - rmean[c] * sc;
 }
 
+// eval-mode BatchNorm inside the train-structured forward (gradients through model.eval()): the coefficients of
+// bn_eval_coeffs_kernel and, for a fused (BN-ReLU staged) layer under h3, the exact max of z = relu(y s + t) from the
+// conv epilogue's per-channel max / min keys (as bn_fwd_finalize_kernel); running statistics untouched
+__global__ void bn_frozen_fwd_kernel(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                                     float eps, float* mean, float* invstd, float* scale, float* shift, const int* ymm,
+                                     int ymm_ld, float* amax_z) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float is = 1.0f / sqrtf(rvar[c] + eps);
+    const float sc = gamma[c] * is, sh = beta[c] - rmean[c] * sc;
+    mean[c] = rmean[c]; invstd[c] = is; scale[c] = sc; shift[c] = sh;
+    if (ymm) {
+        const float yx = sc >= 0.f ? fkey_inv(ymm[c]) : fkey_inv(ymm[ymm_ld + c]);
+        atomicMax(reinterpret_cast<unsigned*>(amax_z), __float_as_uint(relu_f(fmaf(yx, sc, sh))));
+    }
+}
+
 // GroupNorm: block per image n; partials slab[n][nchunks][R][C].
 // one block per (sample n, group g): the group's (chunk, channel) partials strided over 256 threads, fp64, then a
 // fixed-order tree (deterministic).  (One thread per group walking every chunk took ~1 ms per launch at C5's
@@ -286,9 +303,11 @@ __global__ __launch_bounds__(256) void gn_fwd_finalize_kernel(const float* slab,
 }
 
 // BatchNorm backward: dgamma/dbeta (assign), dy = A*gpre + B + Cc*xhat coefficients, conv bias grad.
+// frozen (eval-mode BatchNorm, running statistics): y_hat does not depend on the batch, so dy = gamma invstd g_pre only
+// (A = gamma invstd, B = Cc = 0) and dbias = A S1 — the backward of torch's batch_norm(training=False)
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* part, int S, int C, double count,
                                        const float* gamma, const float* invstd, float* dgamma, float* dbeta, float* A,
-                                       float* B, float* Cc, float* dbias) {
+                                       float* B, float* Cc, float* dbias, int frozen) {
     __shared__ double r1[16][17], r2[16][17], r5[16][17];
     const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
     const int c = blockIdx.x * 16 + cl;
@@ -319,7 +338,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* part
 #pragma unroll
     for (int k = 0; k < 16; ++k) { s1 += r1[k][cl]; s2 += r2[k][cl]; s5 += r5[k][cl]; }
     const double a = (double)gamma[c] * (double)invstd[c];
-    const double b = -a * s1 / count, cc = -a * s2 / count;
+    const double b = frozen ? 0.0 : -a * s1 / count, cc = frozen ? 0.0 : -a * s2 / count;
     dgamma[c] = (float)s2; dbeta[c] = (float)s1;
     A[c] = (float)a; B[c] = (float)b; Cc[c] = (float)cc;
     if (dbias) dbias[c] = (float)(a * s1 + b * count + cc * s5);
@@ -676,6 +695,14 @@ CDM_API int cdm_fill_i32(int* p, long long n, int v, void* stream) {
     return cdm_status();
 }
 
+CDM_API int cdm_bn_fwd_frozen(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                              float eps, float* mean, float* invstd, float* scale, float* shift, const int* ymm,
+                              int ymm_ld, float* amax_z, void* stream) {
+    if (ymm && !amax_z) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_frozen_fwd_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), C, gamma, beta, rmean, rvar,
+                       eps, mean, invstd, scale, shift, ymm, ymm_ld, amax_z);
+    return cdm_status();
+}
 CDM_API int cdm_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
                                float eps, float* mean, float* invstd, float* scale, float* shift, void* stream) {
     hipLaunchKernelGGL(bn_eval_coeffs_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), C, gamma, beta, rmean, rvar,
@@ -697,7 +724,14 @@ CDM_API int cdm_bn_bwd_finalize(const double* part, int nparts, int C, double co
                                 const float* invstd, float* dgamma, float* dbeta, float* A, float* B, float* Cc,
                                 float* dbias, void* stream) {
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, S(stream), part, nparts, C, count,
-                       gamma, invstd, dgamma, dbeta, A, B, Cc, dbias);
+                       gamma, invstd, dgamma, dbeta, A, B, Cc, dbias, 0);
+    return cdm_status();
+}
+CDM_API int cdm_bn_bwd_finalize_frozen(const double* part, int nparts, int C, double count, const float* gamma,
+                                       const float* invstd, float* dgamma, float* dbeta, float* A, float* B, float* Cc,
+                                       float* dbias, void* stream) {
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, S(stream), part, nparts, C, count,
+                       gamma, invstd, dgamma, dbeta, A, B, Cc, dbias, 1);
     return cdm_status();
 }
 

@@ -138,6 +138,11 @@ class UNetEngine:
         # (concatenation slices, pool / FiLM / residual outputs, the C_in = 1 init conv) stay fp32.
         # $CDM_ACT16=0 keeps fp32 activations (A/B checks).
         self.act16 = self.nterm == 1 and os.environ.get("CDM_ACT16", "1") != "0"
+        # a fused layer's dgrad also stores the dy its staging computes (the BN backward of g), and the weight gradient
+        # stages that dy instead of evaluating the BN backward again in each of its 3 kernel-row blocks
+        # ($CDM_DY_STORE=0 / 1; same-box A/B, 2 runs each: C4 29.64-29.89 -> 29.02-29.04 ms per step, C2 50.57-50.62 ->
+        # 50.36-50.37 ms, profiles/r4_ab_dy_store_ks4.txt)
+        self.dy_store = self.x16 and os.environ.get("CDM_DY_STORE", "1") == "1"
         self.device = torch.device(device)
         self.layers = conv_layers(n_feat, height)
         self.L = {l.name: l for l in self.layers}
@@ -401,15 +406,20 @@ class UNetEngine:
     # forward
     # ------------------------------------------------------------------------------------------
     def forward(self, ws: "Workspace", P, x: torch.Tensor, t_in: torch.Tensor, c_in: Optional[torch.Tensor],
-                sc_w: torch.Tensor, sc_b: torch.Tensor, sc_split: int, stream: int, out: Optional[torch.Tensor] = None):
+                sc_w: torch.Tensor, sc_b: torch.Tensor, sc_split: int, stream: int, out: Optional[torch.Tensor] = None,
+                frozen: bool = False):
         """x [B,H,W] fp32 (C=1, NCHW == NHWC), t_in [rows_t] (rows 1 or B), c_in [rows_c, ncf] or None (zeros).
 
         sc_w/sc_b: shortcut 1x1 conv weights, [2, nf] when sc_split < B (CFG halves) else [nf]-shaped.
+        frozen (train-mode workspace only): BatchNorm with the running statistics, not updated — the forward of
+        model.eval() kept for a backward (backward(..., frozen=True)).
         Returns eps [B, H, W] (written into ``out`` when given)."""
         lb = lib(); s = stream
         nf, H, B = self.nf, self.H, ws.B
         H1, H2 = H // 2, H // 4
         train = ws.train
+        assert train or not frozen
+        ws.frozen = frozen
         eps = out if out is not None else ws.eps
         ws.x_in = x
         ws.sc_pending = (sc_w, sc_b, sc_split)
@@ -526,11 +536,17 @@ class UNetEngine:
             nparts = fold(ws, _p(ws.slab), ntiles, 2, l.cout, s)
             fused_fwd = l.name in ws.fused_fwd
             ymm_p, ymm_ld = ws.ymm_of(l) if (fused_fwd and self.h3) else (None, 0)
-            lb.cdm_bn_fwd_finalize(_p(ws.dpart), nparts, 2, l.cout, float(npix), _p(P[bn + ".weight"]),
-                                   _p(P[bn + ".bias"]), _p(P[bn + ".running_mean"]), _p(P[bn + ".running_var"]),
-                                   _p(P[bn + ".num_batches_tracked"]), BN_MOM, BN_EPS, _p(st["mean"]),
-                                   _p(st["invstd"]), _p(st["scale"]), _p(st["shift"]), ymm_p, ymm_ld,
-                                   self._dst_slot(ws, l) if fused_fwd else None, s)
+            if ws.frozen:
+                lb.cdm_bn_fwd_frozen(l.cout, _p(P[bn + ".weight"]), _p(P[bn + ".bias"]), _p(P[bn + ".running_mean"]),
+                                     _p(P[bn + ".running_var"]), BN_EPS, _p(st["mean"]), _p(st["invstd"]),
+                                     _p(st["scale"]), _p(st["shift"]), ymm_p, ymm_ld,
+                                     self._dst_slot(ws, l) if fused_fwd else None, s)
+            else:
+                lb.cdm_bn_fwd_finalize(_p(ws.dpart), nparts, 2, l.cout, float(npix), _p(P[bn + ".weight"]),
+                                       _p(P[bn + ".bias"]), _p(P[bn + ".running_mean"]), _p(P[bn + ".running_var"]),
+                                       _p(P[bn + ".num_batches_tracked"]), BN_MOM, BN_EPS, _p(st["mean"]),
+                                       _p(st["invstd"]), _p(st["scale"]), _p(st["shift"]), ymm_p, ymm_ld,
+                                       self._dst_slot(ws, l) if fused_fwd else None, s)
             if fused_fwd:
                 return                    # z = relu(y s + t) is applied by the next conv's staging
             scale, shift, relu = st["scale"], st["shift"], APPLY_RELU
@@ -757,9 +773,9 @@ class UNetEngine:
                 lb.cdm_slab_sum_nc(_p(ws.slab), B, nch, 5, 2, C, _p(ws.d_emb["contextembed2"]), s)
                 lb.cdm_slab_sum_nc(_p(ws.slab), B, nch, 5, 3, C, _p(ws.d_emb["timeembed2"]), s)
             nparts = fold(ws, _p(ws.slab), B * nch, 5, C, s)
-        lb.cdm_bn_bwd_finalize(_p(ws.dpart), nparts, C, float(B * S * S), _p(P[bn + ".weight"]), _p(st["invstd"]),
-                               _p(G[bn + ".weight"]), _p(G[bn + ".bias"]), _p(co[0]), _p(co[1]), _p(co[2]),
-                               _p(G[l.b]), s)
+        fin = lb.cdm_bn_bwd_finalize_frozen if ws.frozen else lb.cdm_bn_bwd_finalize
+        fin(_p(ws.dpart), nparts, C, float(B * S * S), _p(P[bn + ".weight"]), _p(st["invstd"]), _p(G[bn + ".weight"]),
+            _p(G[bn + ".bias"]), _p(co[0]), _p(co[1]), _p(co[2]), _p(G[l.b]), s)
         gslot = self._dgrad_amax_slot(ws, l)
         if l.name in ws.fused:
             # dy = bn_bwd(g, y) inside the staging of both convs; its scale from a bound on max|dy|
@@ -775,6 +791,24 @@ class UNetEngine:
             dgd = ws.dgrad_dst[l.name]
             key = l.name + ".wdg"
             own16 = 1 if l.name in ws.act16 else 0
+            if ws.dyo is not None:
+                # the dgrad stores dy; the weight gradient stages it (no BN backward there)
+                lb.cdm_conv3x3_dgrad_x16_bnbwd_dy(g.p, g.ld, _p(y), C, *coef, B, S, S, C, _p(self.pk[key + "_x"]),
+                                                  dslot, self._wamax(key), dgd.p, dgd.ld, l.cin,
+                                                  EPI_ACCUM if ws.dgrad_accum[l.name] else 0, gslot, _p(ws.dyo),
+                                                  self.nterm, own16 | self._dgrad_out16(ws, l), s)
+                nul = (None,) * 7
+                if pre is None:
+                    lb.cdm_conv3x3_wgrad_x16_ex(_p(ws.dyo), g.ld, None, 0, *nul, C, src.p, B, S, S, l.cin, src.ld, None,
+                                                None, None, 0, None, None, None, dslot, self._src_slot(ws, l), sp,
+                                                _p(ws.slab), self.nterm, own16, s)
+                else:
+                    lb.cdm_conv3x3_wgrad_x16_ex(_p(ws.dyo), g.ld, None, 0, *nul, C, src.p, B, S, S, l.cin, src.ld,
+                                                pre[0], pre[1], *self._producer_sums(ws, l, sp), dslot,
+                                                self._src_slot(ws, l), sp, _p(ws.slab), self.nterm,
+                                                own16 | self._prod16(ws, l), s)
+                lb.cdm_slab_reduce(_p(ws.slab), sp, C, 9 * l.cin, _p(G[l.w]), 9 * l.cin, 1, 9, l.cin, 0, 1.0, s)
+                return
             lb.cdm_conv3x3_dgrad_x16_bnbwd(g.p, g.ld, _p(y), C, *coef, B, S, S, C, _p(self.pk[key + "_x"]), dslot,
                                            self._wamax(key), dgd.p, dgd.ld, l.cin,
                                            EPI_ACCUM if ws.dgrad_accum[l.name] else 0, gslot, self.nterm,
@@ -999,6 +1033,7 @@ class Workspace:
 
     def __init__(self, eng: UNetEngine, B: int, train: bool):
         self.eng, self.B, self.train = eng, B, train
+        self.frozen = False          # set by each forward (eval-mode BatchNorm in a train-structured forward)
         dev = eng.device
         nf, H, ncf = eng.nf, eng.H, eng.ncf
         H1, H2 = H // 2, H // 4
@@ -1121,6 +1156,11 @@ class Workspace:
                 elif l.cin > 1:
                     self.dgrad_dst[l.name], self.dgrad_accum[l.name] = Act(Gb, l.cin), False
             self._wire_fused_bn_bwd(eng, L, kinds)
+            # the fused layers' dy (eng.dy_store): one buffer, rewritten by each fused layer's dgrad and read by its
+            # weight gradient right after; g's row stride (fp32 size, bf16 dy use half)
+            self.dyo = None
+            if eng.dy_store and self.fused:
+                self.dyo = E(max(B * l.S * l.S * self.gout[l.name].ld for l in L if l.name in self.fused))
             # producer BN-backward sums in the consumer's weight gradient: a fused (BN-ReLU staged) dense producer p
             # whose consumer c takes the kernel-row weight gradient with the X transform
             self.sums_from, self.sums_by, self.sums_sp = {}, {}, {}
@@ -1144,6 +1184,7 @@ class Workspace:
             self.fused, self.g_amax_key, self.out0_g_key = set(), {}, None
             self.sums_from, self.sums_by, self.sums_sp = {}, {}, {}
             self.act16 = set()
+            self.dyo = None
 
     def ymm_of(self, l) -> tuple:
         """(pointer, ld) of fused layer l's max keys; its min keys sit ld ints further."""

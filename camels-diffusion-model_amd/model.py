@@ -135,13 +135,15 @@ class _UNetFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, holder, x, t, c, sc_w, sc_b, *params):
         mod: "ContextUnet" = holder[0]
+        frozen = holder[1]          # eval mode: BatchNorm on the running statistics (batch_norm(training=False))
         eng, P = mod._engine_and_params()
         s = _stream()
         B = x.shape[0]
         eng.repack(P, True, s)
         ctx.pack_token = eng.train_pack_token = object()   # whose weights the engine's train pack holds
         ws = eng.workspace(B, True)
-        eps = eng.forward(ws, P, x.reshape(B, mod.h, mod.h), t, c, sc_w, sc_b, B, s)
+        eps = eng.forward(ws, P, x.reshape(B, mod.h, mod.h), t, c, sc_w, sc_b, B, s, frozen=frozen)
+        ctx.frozen = frozen
         mod._invalidate_eval_pack()
         ctx.state = (mod, eng, ws, P)
         # the engine backward reads the live parameters (BatchNorm weights, ConvT / EmbedFC weights): saved so that
@@ -165,23 +167,11 @@ class _UNetFunction(torch.autograd.Function):
         dx = torch.empty(ws.B, mod.h, mod.h, device=dev) if need_x else None
         dt = torch.empty(ws.t_rows, device=dev) if need_t else None
         dc = torch.empty(ws.c_rows, mod.n_cfeat, device=dev) if need_c else None
+        ws.frozen = ctx.frozen
         eng.backward(ws, P, geps.reshape(ws.B, mod.h, mod.h).contiguous(), G, _stream(), dx=dx, dt=dt, dc=dc)
         ctx.state = None
         return (None, None if dx is None else dx.view(ws.B, 1, mod.h, mod.h), dt, dc, None, None,
                 *[G[n] for n in names])
-
-
-class _EvalNoBackward(torch.autograd.Function):
-    """Carries an eval-mode forward's output in an autograd graph whose backward raises."""
-
-    @staticmethod
-    def forward(ctx, eps, *params):
-        return eps.view_as(eps)
-
-    @staticmethod
-    def backward(ctx, *grads):
-        raise NotImplementedError("gradients through eval-mode BatchNorm are not implemented on the HIP engine "
-                                  "(the reference trains in train mode); use model.train() to differentiate")
 
 
 class ContextUnet(nn.Module):
@@ -271,8 +261,12 @@ class ContextUnet(nn.Module):
         sc_w, sc_b = self.draw_shortcut(dev)
         needs_grad = torch.is_grad_enabled() and (any(p.requires_grad for p in self.parameters())
                                                   or any(v is not None and v.requires_grad for v in (x, t, c)))
-        if self.training and needs_grad:
-            return _UNetFunction.apply((self,), x, t, c, sc_w, sc_b, *[P[n] for n in self._param_names])
+        if needs_grad:
+            # train mode: batch statistics (and the running-stat update); eval mode under autograd: the same
+            # train-structured forward with BatchNorm frozen on the running statistics, differentiable like the
+            # reference's eval() module
+            return _UNetFunction.apply((self, not self.training), x, t, c, sc_w, sc_b,
+                                       *[P[n] for n in self._param_names])
         s = _stream()
         train = self.training
         if train:
@@ -284,10 +278,6 @@ class ContextUnet(nn.Module):
         ws = _cached_ws(eng, B, train)
         eps = torch.empty(B, 1, self.h, self.h, device=dev)
         eng.forward(ws, P, x.reshape(B, self.h, self.h), t, c, sc_w, sc_b, B, s, out=eps.view(B, self.h, self.h))
-        if needs_grad:
-            # model.eval(); model(x, t, c) outside torch.no_grad() works in the reference; the forward here is
-            # the same, and only an actual backward through eval-mode BatchNorm (off the reference's hot path) raises
-            return _EvalNoBackward.apply(eps, *[P[n] for n in self._param_names])
         return eps
 
 

@@ -121,6 +121,14 @@ int cdm_conv3x3_dgrad_x16_bnbwd(const float* g, int ldg, const float* y, int ldy
                                 int N, int H, int W, int C, const void* wx, const float* amax_dy, const float* amax_w,
                                 float* out, int ldo, int Cout, int flags, float* amax_out, int nterm, int dt,
                                 void* stream);
+/* the same, also storing the dy it computes into dy_out ([pix][C], g's row stride ldg and element type) for the
+ * layer's weight gradient (cdm_conv3x3_wgrad_x16_ex with g = dy_out, y = null): the BN backward is evaluated once per
+ * element instead of again in each of the weight gradient's 3 kernel-row blocks. */
+int cdm_conv3x3_dgrad_x16_bnbwd_dy(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
+                                   const float* mean, const float* invstd, const float* A, const float* B,
+                                   const float* Cc, int N, int H, int W, int C, const void* wx, const float* amax_dy,
+                                   const float* amax_w, float* out, int ldo, int Cout, int flags, float* amax_out,
+                                   void* dy_out, int nterm, int dt, void* stream);
 int cdm_conv3x3_wgrad_x16_bnbwd(const float* g, int ldg, const float* y, int ldy, const float* s, const float* t,
                                 const float* mean, const float* invstd, const float* A, const float* B, const float* Cc,
                                 int Cout, const float* x, int N, int H, int W, int Cin, int ldx, const float* amax_dy,
@@ -248,6 +256,16 @@ int cdm_gn_fwd_finalize(const float* slab, int N, int nchunks, int R, int C, int
                         void* stream);
 int cdm_bn_bwd_finalize(const double* part, int nparts, int C, double count, const float* gamma, const float* invstd,
                         float* dgamma, float* dbeta, float* A, float* B, float* Cc, float* dbias, void* stream);
+/* eval-mode BatchNorm in the train-structured forward / backward (gradients through model.eval(), the reference's
+ * batch_norm(training=False) under autograd): coefficients from the running statistics (running stats and
+ * num_batches_tracked untouched; ymm / amax_z as cdm_bn_fwd_finalize), and the backward finalize with the batch terms
+ * dropped (A = gamma invstd, B = Cc = 0, dgamma = S2, dbeta = S1, dbias = A S1) */
+int cdm_bn_fwd_frozen(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
+                      float* mean, float* invstd, float* scale, float* shift, const int* ymm, int ymm_ld, float* amax_z,
+                      void* stream);
+int cdm_bn_bwd_finalize_frozen(const double* part, int nparts, int C, double count, const float* gamma,
+                               const float* invstd, float* dgamma, float* dbeta, float* A, float* B, float* Cc,
+                               float* dbias, void* stream);
 int cdm_gn_bwd_finalize(const float* slab, int N, int nchunks, int C, int G, double count_g, int HW,
                         const float* gamma, const float* invstd, float* A, float* B, float* Cc, float* pdg, float* pdb,
                         float* pdbias, void* stream);

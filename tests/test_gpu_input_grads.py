@@ -30,8 +30,8 @@ def _rel_l2(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
 
 
-def _oracle(sd, x, t, c, sc, dtype, weight):
-    """autograd of the oracle forward (train mode) -> (eps, dx, dt, dc, param grads)."""
+def _oracle(sd, x, t, c, sc, dtype, weight, train=True):
+    """autograd of the oracle forward (train / eval BatchNorm) -> (eps, dx, dt, dc, param grads)."""
     sd = {k: (v.to(dtype) if v.is_floating_point() else v.clone()).clone() for k, v in sd.items()}
     keys = [k for k, _, kind in R.state_dict_layout(1, NF, NCF, H) if kind == "param"]
     for k in keys:
@@ -39,7 +39,7 @@ def _oracle(sd, x, t, c, sc, dtype, weight):
     xx = x.to(dtype).clone().requires_grad_(True)
     tt = t.to(dtype).clone().requires_grad_(True)
     cc = c.to(dtype).clone().requires_grad_(True)
-    eps = R.unet_forward(sd, xx, tt, cc, n_feat=NF, n_cfeat=NCF, height=H, train=True,
+    eps = R.unet_forward(sd, xx, tt, cc, n_feat=NF, n_cfeat=NCF, height=H, train=train,
                          shortcut=(sc[0].to(dtype), sc[1].to(dtype)))
     (eps * weight.to(dtype)).sum().backward()
     return eps.detach(), xx.grad, tt.grad, cc.grad, {k: sd[k].grad for k in keys}
@@ -193,3 +193,52 @@ def test_two_models_interleaved_backward():
         grads.append({k: p.grad.clone() for k, p in a.named_parameters()})
     for k in grads[0]:
         assert torch.equal(grads[0][k], grads[1][k]), k
+
+
+@pytest.mark.parametrize("math", ["fp32", "h3"])
+def test_eval_mode_grads_vs_autograd(math):
+    """Gradients through model.eval() (BatchNorm on the running statistics, batch_norm(training=False) under autograd:
+    dy = gamma invstd g_pre, no batch terms), input and parameter gradients, against the oracle's autograd in eval mode
+    (fp64 truth, same bar as test_input_grads_vs_autograd).  Running statistics made non-trivial by two train forwards
+    first; they must not move during the eval forward / backward."""
+    import cdm_amd
+    torch.manual_seed(3 + 100 * KINK_FREE_SEED)
+    m = cdm_amd.ContextUnet(1, NF, NCF, H, conv_math=math).cuda().train()
+    g = torch.Generator().manual_seed(11 + 100 * KINK_FREE_SEED)
+    with torch.no_grad():
+        for _ in range(2):
+            m(torch.randn(B, 1, H, H, generator=g).cuda(), torch.rand(B, generator=g).cuda(),
+              torch.rand(B, NCF, generator=g).cuda())
+    m.eval()
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    x = torch.randn(B, 1, H, H, generator=g)
+    t = torch.rand(B, generator=g)
+    c = torch.rand(B, NCF, generator=g)
+    weight = torch.randn(B, 1, H, H, generator=g)
+    torch.manual_seed(21)
+    sc = R.draw_shortcut(1, NF)
+    xg, tg, cg = (v.cuda().requires_grad_(True) for v in (x, t, c))
+    torch.manual_seed(21)
+    eps = m(xg, tg, cg)
+    (eps * weight.cuda()).sum().backward()
+    for k, v in m.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            assert torch.equal(v.cpu(), sd[k]), k
+    e64, dx64, dt64, dc64, g64 = _oracle(sd, x, t, c, sc, torch.float64, weight, train=False)
+    e32, dx32, dt32, dc32, g32 = _oracle(sd, x, t, c, sc, torch.float32, weight, train=False)
+    assert _rel_l2(eps.detach(), e64) <= 3 * _rel_l2(e32, e64) + 2e-6
+    rec, bad = {}, []
+    hip_p = dict(m.named_parameters())
+    items = [("x", xg.grad.view(B, 1, H, H), dx64, dx32), ("t", tg.grad, dt64, dt32), ("c", cg.grad, dc64, dc32)]
+    items += [(k, hip_p[k].grad, g64[k], g32[k]) for k in g64]
+    for name, hip, r64, r32 in items:
+        assert hip is not None, name
+        if r64.norm() == 0:
+            continue
+        eh, er = _rel_l2(hip, r64), _rel_l2(r32, r64)
+        rec[name] = (eh, er)
+        if eh > 3 * er + 2e-6:
+            bad.append((name, eh, er))
+    _parity.record("eval_mode_grads", conv_math=math, worst=sorted(rec.items(), key=lambda kv: -kv[1][0])[:5])
+    print(f"[{math}] eval-mode gradients: worst", sorted(rec.items(), key=lambda kv: -kv[1][0])[:4])
+    assert not bad, bad

@@ -400,6 +400,13 @@ def test_bn_bwd_fused_into_conv_staging_bit_exact(L, N, S, C, Cin):
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
     assert a1[0].item() == a1[1].item() == ref.abs().max().item()
+    # the same dgrad also storing the dy it stages (each element once, for the weight gradient): dy bit for bit
+    dyo = torch.full((P, C), float("nan"), device="cuda"); got2 = torch.empty_like(got)
+    L.cdm_conv3x3_dgrad_x16_bnbwd_dy(gr.data_ptr(), C, y.data_ptr(), C, *coefs, N, S, S, C, wx.data_ptr(), dslot,
+                                     amw.data_ptr(), got2.data_ptr(), Cin, Cin, 0, None, dyo.data_ptr(), 4, 0, _s())
+    torch.cuda.synchronize()
+    assert torch.equal(got2, ref)
+    assert torch.equal(dyo, dy)
     # wgrad of the conv Cin -> C that produced y: dW[co=C][tap*Cin+ci]
     amx = _amax(L, x, P, Cin)
     sp = wgrad_splits(P, C, 9 * Cin)

@@ -238,11 +238,14 @@ def test_fused_bn_bwd_matches_unfused_nf128():
 
 
 def test_eval_forward_under_grad_mode():
-    """model.eval(); model(x, t, c) outside torch.no_grad() works as in the reference (same output as under
-    no_grad); only a backward through eval-mode BatchNorm raises."""
+    """model.eval(); model(x, t, c) outside torch.no_grad() works as in the reference and is differentiable: the
+    train-structured forward with BatchNorm frozen on the running statistics (its gradients:
+    tests/test_gpu_input_grads.py::test_eval_mode_grads_vs_autograd).  Same output as the folded no_grad eval path up
+    to fp32 rounding, running statistics untouched, and a backward that runs."""
     fx = _fx("model_nf8.npz")
     m = _model(8, sd=_sd(fx)).eval()
     x, t, c = (torch.from_numpy(fx[k]).cuda() for k in ("x", "t", "c"))
+    run0 = {k: v.clone() for k, v in m.state_dict().items() if "running" in k or "num_batches" in k}
     torch.manual_seed(11)
     out = m(x, t, c)
     assert out.requires_grad
@@ -250,9 +253,12 @@ def test_eval_forward_under_grad_mode():
     torch.manual_seed(11)
     with torch.no_grad():
         ref = m(x, t, c)
-    assert torch.equal(out.detach(), ref)
-    with pytest.raises(NotImplementedError):
-        out.sum().backward()
+    assert _rel(out.detach(), ref) < 1e-5
+    out.sum().backward()
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())
+    for k, v in m.state_dict().items():
+        if k in run0:
+            assert torch.equal(v, run0[k]), k
 
 
 @pytest.mark.parametrize("B", [2, 5])
