@@ -177,7 +177,7 @@ enum { EPI_RELU = 1, EPI_ACCUM = 2 };
 
 // WM = waves along M (2: 128-row block, 4: 256-row block); stats per 128-row tile.  OT = the stored element type (bf16:
 // C4's fused-chain activations and gradients; the statistics / maxima are those of the stored, rounded values)
-template <int WM = 2, class OT = float>
+template <int WM = 2, class OT = float, bool ACC = false>
 struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-tile column stats
     OT* y; long long ldy; long long zstride; const float* bias; int bias_mod; int flags;
     float* stats; int stats_ld;  // stats[tile][0|1][stats_ld]: sum / sum of squares of the stored value
@@ -199,16 +199,46 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
             for (int j = 0; j < 2; ++j) bj[j] = bias ? bias[(nw + 32 * j + (lane & 31)) % bias_mod] : 0.f;
             const bool relu = flags & EPI_RELU;
             const bool accum = flags & EPI_ACCUM;
-            CDM_FOR_ACC({
-                float v = acc[i][j][r] + bj[j];
-                if (accum) v += Act<OT>::load(yz + (long long)m * ldy + n);
-                if (relu) v = relu_f(v);
-                v = Act<OT>::round(v);
-                Act<OT>::store(yz + (long long)m * ldy + n, v);
-                cs[j] += v; cq[j] += v * v;
-                am = fmaxf(am, fabsf(v));
-                cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
-            })
+            if constexpr (ACC) {
+                // accumulate (a compile-time variant: the interleaved form below waited on one load per element — the
+                // compiler cannot prove the addresses disjoint — +0.5 ms per accumulating 64^2 dgrad, profiles/
+                // r4_train_step_sequence_c2.txt; holding the old values in the shared epilogue made every conv spill):
+                // the 16 old values of a 32 x 32 block are loaded before its first store
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        float old[16];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = mw + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                            old[r] = Act<OT>::load(yz + (long long)m * ldy + nw + 32 * j + (lane & 31));
+                        }
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = mw + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                            const int n = nw + 32 * j + (lane & 31);
+                            float v = acc[i][j][r] + bj[j] + old[r];
+                            if (relu) v = relu_f(v);
+                            v = Act<OT>::round(v);
+                            Act<OT>::store(yz + (long long)m * ldy + n, v);
+                            cs[j] += v; cq[j] += v * v;
+                            am = fmaxf(am, fabsf(v));
+                            cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
+                        }
+                    }
+            } else {
+                CDM_FOR_ACC({
+                    float v = acc[i][j][r] + bj[j];
+                    if (accum) v += Act<OT>::load(yz + (long long)m * ldy + n);
+                    if (relu) v = relu_f(v);
+                    v = Act<OT>::round(v);
+                    Act<OT>::store(yz + (long long)m * ldy + n, v);
+                    cs[j] += v; cq[j] += v * v;
+                    am = fmaxf(am, fabsf(v));
+                    cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
+                })
+            }
         } else {
             CDM_FOR_ACC({
                 if (m < M && n < N) {
@@ -282,7 +312,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
 };
 using EpiStore = EpiStoreW<2>;
 template <class EP> struct IsEpiStoreW : std::false_type {};
-template <int WM, class OT> struct IsEpiStoreW<EpiStoreW<WM, OT>> : std::true_type {};
+template <int WM, class OT, bool ACC> struct IsEpiStoreW<EpiStoreW<WM, OT, ACC>> : std::true_type {};
 
 struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n, 2h+i, 2w+j, co] = acc + b[co]
     float* y; long long ldy; const float* bias; int H, W, Co, M, N;
@@ -1896,11 +1926,11 @@ static int halo_deep() {
 
 // XT / OT: element types of the source (x, PRE's y) and of the stored output; bf16 only with the one-term (C4)
 // arithmetic
-template <int WT, class PRE = PreNone, class XT = float, class OT = float>
+template <int WT, class PRE = PreNone, class XT = float, class OT = float, bool ACC = false>
 static int launch_conv_halo(const XT* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
-                            const float* amax_x, const float* amax_w, const EpiStoreW<4, OT>& ep, int nterm, hipStream_t s,
-                            PRE pre = PRE{}, int tpb = 0) {
-    using EP = EpiStoreW<4, OT>;
+                            const float* amax_x, const float* amax_w, const EpiStoreW<4, OT, ACC>& ep, int nterm,
+                            hipStream_t s, PRE pre = PRE{}, int tpb = 0) {
+    using EP = EpiStoreW<4, OT, ACC>;
     constexpr bool F32 = std::is_same<XT, float>::value && std::is_same<OT, float>::value;
     const int M = N * H * WT, mtiles = M / HBM_;
     // the kernel addresses the halo sources (x, pre.y) by 32-bit byte offsets from their base
@@ -1961,10 +1991,19 @@ static int launch_conv_halo(const XT* x, int N, int H, int Cin, int ldx, const _
 }
 
 // LDS-halo conv of a W x W image (W in {32, 64}; 128 / 256 with the h3 arithmetic only)
-template <class PRE = PreNone, class XT = float, class OT = float>
+template <class PRE = PreNone, class XT = float, class OT = float, bool ACC = false>
 static int launch_conv_halo_w(int W, const XT* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
-                              const float* amax_x, const float* amax_w, const EpiStoreW<4, OT>& ep, int nterm,
+                              const float* amax_x, const float* amax_w, const EpiStoreW<4, OT, ACC>& ep, int nterm,
                               hipStream_t s, PRE pre = PRE{}) {
+    if constexpr (ACC) {   // the accumulating (load-ahead epilogue) variant: the dgrads at 32^2 / 64^2 only
+        switch (W) {
+            case 32: return launch_conv_halo<32, PRE, XT, OT, ACC>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm,
+                                                                   s, pre);
+            case 64: return launch_conv_halo<64, PRE, XT, OT, ACC>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm,
+                                                                   s, pre);
+            default: return (int)hipErrorInvalidValue;
+        }
+    } else {
     switch (W) {
         case 32: return launch_conv_halo<32, PRE, XT, OT>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
         case 64: return launch_conv_halo<64, PRE, XT, OT>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
@@ -1973,6 +2012,7 @@ static int launch_conv_halo_w(int W, const XT* x, int N, int H, int Cin, int ldx
             if constexpr (PRE::on) return (int)hipErrorInvalidValue;
             else return launch_conv_halo<256, PRE, XT, OT>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm, s, pre);
         default: return (int)hipErrorInvalidValue;
+    }
     }
 }
 static bool halo_width_ok(int W, int nterm) {
@@ -2236,10 +2276,16 @@ static int conv3x3_fwd_split(const float* x, int N, int H, int W, int Cin, int l
         auto run = [&](auto xtag, auto otag) {
             using XT = decltype(xtag);
             using OT = decltype(otag);
-            EpiStoreW<4, OT> eh{reinterpret_cast<OT*>(y), ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
-            eh.ymm = ymm; eh.ymm_ld = ymm_ld;
             const __bf16* b = reinterpret_cast<const __bf16*>(wx);
             const XT* xx = reinterpret_cast<const XT*>(x);
+            if constexpr (std::is_same<OT, float>::value) {   // an accumulating dgrad: the load-ahead epilogue
+                if ((flags & EPI_ACCUM) && !pre_s && !stats && !ymm && W <= 64) {
+                    const EpiStoreW<4, float, true> ea{y, ldy, 0, bias, Cout, flags, nullptr, 0, M, Cout, amax_y};
+                    return launch_conv_halo_w(W, xx, N, H, Cin, ldx, b, Cout, amax_x, amax_w, ea, nterm, st);
+                }
+            }
+            EpiStoreW<4, OT> eh{reinterpret_cast<OT*>(y), ldy, 0, bias, Cout, flags, stats, stats_ld, M, Cout, amax_y};
+            eh.ymm = ymm; eh.ymm_ld = ymm_ld;
             if (pre_s) return launch_conv_halo_w(W, xx, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st,
                                                  PreBnRelu{{pre_s, pre_t}});
             return launch_conv_halo_w(W, xx, N, H, Cin, ldx, b, Cout, amax_x, amax_w, eh, nterm, st);
@@ -2336,6 +2382,13 @@ CDM_API int cdm_conv3x3_dgrad_x16_bnbwd_dy(const float* g, int ldg, const float*
     auto run = [&](auto xtag, auto otag) {
         using XT = decltype(xtag);
         using OT = decltype(otag);
+        if constexpr (std::is_same<OT, float>::value) {   // an accumulating dgrad: the load-ahead epilogue
+            if ((flags & EPI_ACCUM) && W <= 64) {
+                const EpiStoreW<4, float, true> ea{out, ldo, 0, nullptr, Cout, flags, nullptr, 0, M, Cout, amax_out};
+                return launch_conv_halo_w(W, reinterpret_cast<const XT*>(g), N, H, C, ldg, b, Cout, amax_dy, amax_w, ea,
+                                          nterm, S(stream), pre);
+            }
+        }
         const EpiStoreW<4, OT> eh{reinterpret_cast<OT*>(out), ldo, 0, nullptr, Cout, flags, nullptr, 0, M, Cout,
                                   amax_out};
         return launch_conv_halo_w(W, reinterpret_cast<const XT*>(g), N, H, C, ldg, b, Cout, amax_dy, amax_w, eh, nterm,

@@ -567,9 +567,13 @@ __global__ __launch_bounds__(256) void conv_cout1_dgrad_row_kernel(const float* 
 // A block owns R whole rows of one image; every z pixel q of the band is read from HBM once (float4 per lane,
 // C/4 lanes per pixel: one coalesced row), and its 9 contributions use the deps values around it, staged with a
 // zero border in LDS (no bounds tests).  Per-block partials [9][C] (fixed-order LDS fold over the pixel lanes).
+// gs / gt (optional, per (sample, channel) [N][C]): z = relu(y gs + gt) of the pre-norm y (out.1's GroupNorm + ReLU,
+// the fmaf of norm_apply_fwd: bit-identical to the applied tensor) — z is then never written by the forward
 __global__ __launch_bounds__(256) void conv_cout1_wgrad_band_kernel(const float* __restrict__ deps,
                                                                     const float* __restrict__ z, int ldz, int H, int W,
-                                                                    int C, int R, float* __restrict__ slab) {
+                                                                    int C, int R, float* __restrict__ slab,
+                                                                    const float* __restrict__ gs,
+                                                                    const float* __restrict__ gt) {
     extern __shared__ float sm[];                        // deps band [(R+2)][(W+2)], then the fold [PL][9][C]
     const int bands = H / R, n = blockIdx.x / bands, h0 = (blockIdx.x - n * bands) * R;
     const int C4 = C >> 2, PL = 256 / C4, tid = threadIdx.x, c4 = (tid % C4) * 4, pl = tid / C4;
@@ -586,11 +590,20 @@ __global__ __launch_bounds__(256) void conv_cout1_wgrad_band_kernel(const float*
     for (int t = 0; t < 9; ++t)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[t][j] = 0.f;
+    float ks[4] = {1.f, 1.f, 1.f, 1.f}, kt[4] = {0.f, 0.f, 0.f, 0.f};
+    if (gs) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { ks[j] = gs[n * C + c4 + j]; kt[j] = gt[n * C + c4 + j]; }
+    }
     if (pl < PL) {
         const float* zb = z + ((long long)n * H + h0) * W * ldz + c4;
         for (int q = pl; q < R * W; q += PL) {
             const int r = q / W, c = q - r * W;
-            const float4 v = ld4(zb + (long long)q * ldz);
+            float4 v = ld4(zb + (long long)q * ldz);
+            if (gs) {
+                v.x = relu_f(fmaf(v.x, ks[0], kt[0])); v.y = relu_f(fmaf(v.y, ks[1], kt[1]));
+                v.z = relu_f(fmaf(v.z, ks[2], kt[2])); v.w = relu_f(fmaf(v.w, ks[3], kt[3]));
+            }
             // output pixel p = q - off, off = (ky - 1, kx - 1): deps at band row r + 2 - ky, column c + 2 - kx
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky)
@@ -1180,17 +1193,22 @@ CDM_API int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int 
                        W, C, w, dz, lddz);
     return cdm_status();
 }
+CDM_API int cdm_conv3x3_cout1_wgrad_gn(const float* deps, const float* y, int ldy, int N, int H, int W, int C,
+                                       const float* gs, const float* gt, int csize, float* slab, void* stream) {
+    // band form only: R = -csize whole rows per block, partials [N * H / R][9][C]; gs / gt null: y is z itself
+    if (C % 4 || C > 1024 || csize >= 0 || (gs && !gt)) return (int)hipErrorInvalidValue;
+    const int R = -csize;
+    const size_t lds = (((size_t)(R + 2) * (W + 2) + 3) & ~(size_t)3) * 4 + (size_t)(256 / (C / 4)) * 9 * C * 4;
+    if (H % R || ldy % 4 || lds > 64 * 1024) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(conv_cout1_wgrad_band_kernel, dim3(N * (H / R)), dim3(256), lds, S(stream), deps, y, ldy, H, W, C,
+                       R, slab, gs, gt);
+    return cdm_status();
+}
 CDM_API int cdm_conv3x3_cout1_wgrad(const float* deps, const float* z, int ldz, int N, int H, int W, int C, int csize,
                                     float* slab, void* stream) {
     if (C % 4 || C > 1024) return (int)hipErrorInvalidValue;
-    if (csize < 0) {                  // band form: R = -csize whole rows per block, partials [N * H / R][9][C]
-        const int R = -csize;
-        const size_t lds = (((size_t)(R + 2) * (W + 2) + 3) & ~(size_t)3) * 4 + (size_t)(256 / (C / 4)) * 9 * C * 4;
-        if (H % R || ldz % 4 || lds > 64 * 1024) return (int)hipErrorInvalidValue;
-        hipLaunchKernelGGL(conv_cout1_wgrad_band_kernel, dim3(N * (H / R)), dim3(256), lds, S(stream), deps, z, ldz, H,
-                           W, C, R, slab);
-        return cdm_status();
-    }
+    if (csize < 0)                    // band form: R = -csize whole rows per block, partials [N * H / R][9][C]
+        return cdm_conv3x3_cout1_wgrad_gn(deps, z, ldz, N, H, W, C, nullptr, nullptr, csize, slab, stream);
     hipLaunchKernelGGL(conv_cout1_wgrad_kernel, dim3((H * W + csize - 1) / csize, N), dim3(256), 0, S(stream), deps, z,
                        ldz, H, W, C, csize, slab);
     return cdm_status();

@@ -12,6 +12,8 @@
 // then folded in fp64 by a tiny finalize kernel.  Deterministic: no atomics anywhere.
 #include "cdm_common.h"
 
+#include <type_traits>
+
 namespace cdm {
 
 struct NormP {              // z_pre = y*s + t ; xhat = (y - mean)*invstd
@@ -546,6 +548,46 @@ __global__ __launch_bounds__(256) void norm_apply_bwd_kernel(const float* g, int
     if (amax) block_amax_commit(am, amax);
 }
 
+// dense BatchNorm backward of a bf16-activation (C4) layer as its own pass: dy = bn_bwd_elem(g, y) with the fused
+// staging's expression, g / y of element type GT, dy stored as OT (bf16: the value the fused dgrad staging would have
+// rounded to).  8 channels per thread (16-byte bf16 loads).  The dgrad and weight gradient then stage dy as a plain
+// operand (the LDS-halo forward schedule, halo two chunks ahead, which the fused BN-backward staging cannot hold).
+template <class GT, class OT>
+__global__ __launch_bounds__(256) void bn_bwd_dy_kernel(const GT* __restrict__ g, int ldg, const GT* __restrict__ y,
+                                                        int ldy, long long P, int C, const float* __restrict__ s,
+                                                        const float* __restrict__ t, const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, const float* __restrict__ A,
+                                                        const float* __restrict__ B, const float* __restrict__ Cc,
+                                                        OT* __restrict__ dy, int lddy) {
+    const int C8 = C >> 3;
+    const long long total = P * C8;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int c8 = (int)(idx % C8) * 8;
+        const long long pix = idx / C8;
+        const float4 g0 = Act<GT>::to4(Act<GT>::load4(g + pix * ldg + c8));
+        const float4 g1 = Act<GT>::to4(Act<GT>::load4(g + pix * ldg + c8 + 4));
+        const float4 y0 = Act<GT>::to4(Act<GT>::load4(y + pix * ldy + c8));
+        const float4 y1 = Act<GT>::to4(Act<GT>::load4(y + pix * ldy + c8 + 4));
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = c8 + j;
+            const float gv = j < 4 ? f4get(g0, j) : f4get(g1, j - 4), yv = j < 4 ? f4get(y0, j) : f4get(y1, j - 4);
+            o[j] = bn_bwd_elem(gv, yv, s[c], t[c], mean[c], invstd[c], A[c], B[c], Cc[c]);
+        }
+        OT* d = dy + pix * lddy + c8;
+        if constexpr (std::is_same<OT, float>::value) {
+            st4(d, make_float4(o[0], o[1], o[2], o[3]));
+            st4(d + 4, make_float4(o[4], o[5], o[6], o[7]));
+        } else {
+            typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+            *reinterpret_cast<bf16x8_t*>(d) = bf16x8_t{(__bf16)o[0], (__bf16)o[1], (__bf16)o[2], (__bf16)o[3],
+                                                       (__bf16)o[4], (__bf16)o[5], (__bf16)o[6], (__bf16)o[7]};
+        }
+    }
+}
+
 // upper bound of max|dy| for the fused BN backward (dy never materialised): per channel
 // |A| max|g| + |B| + |Cc| (max|y| + |mean|) invstd >= |A g_pre + B + Cc xhat|; max over channels into *out
 __global__ __launch_bounds__(256) void bn_bwd_amax_bound_kernel(int C, const float* A, const float* B, const float* Cc,
@@ -811,6 +853,29 @@ CDM_API int cdm_norm_apply_bwd(int mode, const float* g, int ldg, const float* y
         hipLaunchKernelGGL((norm_apply_bwd_kernel<false, false>), dim3(nb), dim3(256), 0, S(stream), g, ldg, y, ldy, N, H,
                            W, C, np, fp, A, B, Cc, cn, dy, lddy, amax);
     return cdm_status();
+}
+
+CDM_API int cdm_bn_bwd_dy(const void* g, int ldg, const void* y, int ldy, long long P, int C, const float* s,
+                          const float* t, const float* mean, const float* invstd, const float* A, const float* B,
+                          const float* Cc, void* dy, int lddy, int dt, void* stream) {
+    // dt bit 0: g and y are bf16, bit 1: dy is stored as bf16
+    if (C % 8 || ldg % 8 || ldy % 8 || lddy % 8 || P < 0) return (int)hipErrorInvalidValue;
+    if (P == 0) return 0;
+    const int nb = ew_blocks(P * (C / 8));
+    auto run = [&](auto gtag, auto otag) {
+        using GT = decltype(gtag);
+        using OT = decltype(otag);
+        hipLaunchKernelGGL((bn_bwd_dy_kernel<GT, OT>), dim3(nb), dim3(256), 0, S(stream),
+                           reinterpret_cast<const GT*>(g), ldg, reinterpret_cast<const GT*>(y), ldy, P, C, s, t, mean,
+                           invstd, A, B, Cc, reinterpret_cast<OT*>(dy), lddy);
+        return cdm_status();
+    };
+    switch (dt & 3) {
+        case 1: return run(__bf16{}, float{});
+        case 2: return run(float{}, __bf16{});
+        case 3: return run(__bf16{}, __bf16{});
+        default: return run(float{}, float{});
+    }
 }
 
 CDM_API int cdm_bn_bwd_amax_bound(int C, const float* A, const float* B, const float* Cc, const float* mean,

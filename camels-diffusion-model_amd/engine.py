@@ -143,6 +143,13 @@ class UNetEngine:
         # ($CDM_DY_STORE=0 / 1; same-box A/B, 2 runs each: C4 29.64-29.89 -> 29.02-29.04 ms per step, C2 50.57-50.62 ->
         # 50.36-50.37 ms, profiles/r4_ab_dy_store_ks4.txt)
         self.dy_store = self.x16 and os.environ.get("CDM_DY_STORE", "1") == "1"
+        # bf16 (one-term) arithmetic: dy of a fused layer by a separate elementwise pass (cdm_bn_bwd_dy) and the
+        # dgrad on the plain staging schedule instead of the BN-backward staging ($CDM_DY_PASS=0 / 1; same-box A/B,
+        # 2 runs each: C4 36.72-36.96 -> 34.69-34.70 ms per step, profiles/r4_ab_dy_pass_gn_out.txt)
+        self.dy_pass = self.dy_store and self.nterm == 1 and os.environ.get("CDM_DY_PASS", "1") == "1"
+        # train: out.1's GroupNorm + ReLU inside out.3's forward and weight-gradient staging, zO never written
+        # ($CDM_FUSE_GN_OUT=0: the apply kernel writes zO)
+        self.fuse_gn_out = os.environ.get("CDM_FUSE_GN_OUT", "1") != "0"
         self.device = torch.device(device)
         self.layers = conv_layers(n_feat, height)
         self.L = {l.name: l for l in self.layers}
@@ -489,11 +496,14 @@ class UNetEngine:
                      _p(ws.slab), nf, self.kc_out0, s, amax_x=self._slot(ws, "catO"))
         probe("yO", ws)
         self._gn_fwd(ws, P, "out.1", Act(ws.yO, nf), B, H, nf, ws.gnO, stats_from_conv=True, stream=s)
-        if not train and nf % 16 == 0 and H <= 256 and 256 % H == 0:
-            # eval: out.1's GroupNorm + ReLU applied in out.3's staging (zO is only kept for the backward)
+        if (not train or self.fuse_gn_out) and nf % 16 == 0 and H <= 256 and 256 % H == 0:
+            # out.1's GroupNorm + ReLU applied in out.3's staging (train: and in out.3's weight gradient): zO never
+            # written
             lb.cdm_conv3x3_cout1_fwd_gn(_p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]), _p(ws.gnO["shift"]),
                                         _p(P["out.3.weight"]), _p(P["out.3.bias"]), _p(eps), s)
+            ws.zO_fused = train
             return eps
+        ws.zO_fused = False
         lb.cdm_norm_apply_fwd(APPLY_RELU, _p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]), _p(ws.gnO["shift"]), nf,
                               None, 0, None, 0, None, None, None, 0, _p(ws.zO), nf, None, s)
         lb.cdm_conv3x3_cout1_fwd(_p(ws.zO), nf, B, H, H, nf, _p(P["out.3.weight"]), _p(P["out.3.bias"]), _p(eps), s)
@@ -621,7 +631,11 @@ class UNetEngine:
         P0, P1, P2 = B * H * H, B * H1 * H1, B * H2 * H2
         # ---------------- out.3 (nf -> 1) ----------------
         R = cout1_band_rows(B, H)
-        lb.cdm_conv3x3_cout1_wgrad(_p(deps), _p(ws.zO), nf, B, H, H, nf, -R, _p(ws.slab), s)
+        if ws.zO_fused:
+            lb.cdm_conv3x3_cout1_wgrad_gn(_p(deps), _p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]),
+                                          _p(ws.gnO["shift"]), -R, _p(ws.slab), s)
+        else:
+            lb.cdm_conv3x3_cout1_wgrad(_p(deps), _p(ws.zO), nf, B, H, H, nf, -R, _p(ws.slab), s)
         S = fold(ws, _p(ws.slab), B * H // R, 9, nf, s)
         lb.cdm_slab_sum_all(_p(ws.dpart), S, 9, 0, 9, nf, _p(G["out.3.weight"]), 1, 9, 0, s)
         if not out3_bias_done:
@@ -792,11 +806,19 @@ class UNetEngine:
             key = l.name + ".wdg"
             own16 = 1 if l.name in ws.act16 else 0
             if ws.dyo is not None:
-                # the dgrad stores dy; the weight gradient stages it (no BN backward there)
-                lb.cdm_conv3x3_dgrad_x16_bnbwd_dy(g.p, g.ld, _p(y), C, *coef, B, S, S, C, _p(self.pk[key + "_x"]),
-                                                  dslot, self._wamax(key), dgd.p, dgd.ld, l.cin,
-                                                  EPI_ACCUM if ws.dgrad_accum[l.name] else 0, gslot, _p(ws.dyo),
-                                                  self.nterm, own16 | self._dgrad_out16(ws, l), s)
+                if self.dy_pass:
+                    # bf16 arithmetic: dy by its own elementwise pass, then the dgrad on the LDS-halo forward schedule
+                    # (halo two chunks ahead, one barrier per chunk) — the fused BN-backward staging has no room for it
+                    lb.cdm_bn_bwd_dy(g.p, g.ld, _p(y), C, B * S * S, C, *coef, _p(ws.dyo), g.ld, own16 | (own16 << 1), s)
+                    self.conv3x3(key, _p(ws.dyo), B, S, C, g.ld, None, dgd.p, dgd.ld, l.cin,
+                                 EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s, amax_y=gslot,
+                                 dt=own16 | self._dgrad_out16(ws, l))
+                else:
+                    # the dgrad stores dy; the weight gradient stages it (no BN backward there)
+                    lb.cdm_conv3x3_dgrad_x16_bnbwd_dy(g.p, g.ld, _p(y), C, *coef, B, S, S, C, _p(self.pk[key + "_x"]),
+                                                      dslot, self._wamax(key), dgd.p, dgd.ld, l.cin,
+                                                      EPI_ACCUM if ws.dgrad_accum[l.name] else 0, gslot, _p(ws.dyo),
+                                                      self.nterm, own16 | self._dgrad_out16(ws, l), s)
                 nul = (None,) * 7
                 if pre is None:
                     lb.cdm_conv3x3_wgrad_x16_ex(_p(ws.dyo), g.ld, None, 0, *nul, C, src.p, B, S, S, l.cin, src.ld, None,
@@ -1034,6 +1056,7 @@ class Workspace:
     def __init__(self, eng: UNetEngine, B: int, train: bool):
         self.eng, self.B, self.train = eng, B, train
         self.frozen = False          # set by each forward (eval-mode BatchNorm in a train-structured forward)
+        self.zO_fused = False        # set by each forward: out.1's GroupNorm + ReLU applied inside out.3's kernels
         dev = eng.device
         nf, H, ncf = eng.nf, eng.H, eng.ncf
         H1, H2 = H // 2, H // 4

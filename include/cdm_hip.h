@@ -285,6 +285,12 @@ int cdm_norm_apply_bwd(int mode, const float* g, int ldg, const float* y, int ld
                        float* dy, int lddy, float* amax, void* stream);
 /* *amax_dy = max(*amax_dy, max_c |A| max|g| + |B| + |Cc| (max|y| + |mean|) invstd): an upper bound of max|dy| of
  * the fused BN backward (from the producers' max|g| = *amax_g and max|y| = *amax_y); one block */
+/* dense BatchNorm backward of a bf16-activation (C4) layer as its own pass: dy[p][c] = the fused staging's
+ * bn_bwd_elem(g, y) (s, t, mean, invstd, A, B, Cc per channel), P pixels x C channels (C % 8 == 0); dt bit 0: g and y
+ * are bf16, bit 1: dy is stored as bf16 (round to nearest even) */
+int cdm_bn_bwd_dy(const void* g, int ldg, const void* y, int ldy, long long P, int C, const float* s, const float* t,
+                  const float* mean, const float* invstd, const float* A, const float* B, const float* Cc, void* dy,
+                  int lddy, int dt, void* stream);
 int cdm_bn_bwd_amax_bound(int C, const float* A, const float* B, const float* Cc, const float* mean,
                           const float* invstd, const float* amax_g, const float* amax_y, float* amax_dy, void* stream);
 
@@ -325,6 +331,10 @@ int cdm_conv3x3_cout1_dgrad(const float* deps, int N, int H, int W, int C, const
  * == 0): one block per R whole rows, every z pixel read once, partials [N * H / R][9][C] */
 int cdm_conv3x3_cout1_wgrad(const float* deps, const float* z, int ldz, int N, int H, int W, int C, int csize,
                             float* slab, void* stream);
+/* band form (csize = -R) on out.1's pre-norm output y with its GroupNorm + ReLU (per (n, c) gs / gt, [N][C]) applied
+ * while staging: z = relu(y gs + gt), bit-identical to the applied tensor, never materialised */
+int cdm_conv3x3_cout1_wgrad_gn(const float* deps, const float* y, int ldy, int N, int H, int W, int C, const float* gs,
+                               const float* gt, int csize, float* slab, void* stream);
 /* to_vec: AvgPool2d(h/4) + GELU (ContextUnet.py:17) */
 int cdm_avgpool_gelu_fin(const float* sums, int N, int C, int HW, float* hpre, float* hv, void* stream);
 int cdm_avgpool_gelu_bwd(const float* dhv, const float* hpre, int N, int HW, int C, float* dst, int ldd, void* stream);

@@ -714,3 +714,33 @@ def test_producer_bn_sums_in_wgrad(B, S, cin, cout, nterm):
     err = ((g3 - ref).abs().max(dim=1).values / ref.abs().max(dim=1).values).max().item()
     assert err <= 1e-5, err
     assert float(got[2].abs().max()) == 0 and float(got[3].abs().max()) == 0
+
+
+@pytest.mark.parametrize("dt", [0, 3])
+def test_bn_bwd_dy_pass_bit_exact(L, dt):
+    """cdm_bn_bwd_dy (the C4 layers' separate BN-backward pass) == norm_apply_bwd mode 0 (the expression the fused
+    staging uses) bit for bit: fp32 in / out, and bf16 g / y in, dy rounded to bf16 (round to nearest even)."""
+    g_ = torch.Generator(device="cuda").manual_seed(7)
+    N, S, C = 3, 32, 128
+    P = N * S * S
+    gr = torch.randn(P, C, device="cuda", generator=g_) * 1e-3
+    y = torch.randn(P, C, device="cuda", generator=g_) * 2 + 0.3
+    if dt & 1:
+        gr, y = gr.bfloat16().float(), y.bfloat16().float()
+    co = [torch.randn(C, device="cuda", generator=g_) for _ in range(7)]
+    co[3] = co[3].abs() + 0.1
+    s_, t_, mean, invstd, A, B, Cc = co
+    ref = torch.empty(P, C, device="cuda")
+    L.cdm_norm_apply_bwd(0, gr.data_ptr(), C, y.data_ptr(), C, N, S, S, C, s_.data_ptr(), t_.data_ptr(), 0,
+                         mean.data_ptr(), invstd.data_ptr(), 0, 1, None, 0, A.data_ptr(), B.data_ptr(), Cc.data_ptr(),
+                         0, ref.data_ptr(), C, None, _s())
+    if dt & 1:
+        gi, yi = gr.bfloat16(), y.bfloat16()
+        out = torch.empty(P, C, device="cuda", dtype=torch.bfloat16)
+    else:
+        gi, yi = gr, y
+        out = torch.empty(P, C, device="cuda")
+    L.cdm_bn_bwd_dy(gi.data_ptr(), C, yi.data_ptr(), C, P, C, *[t.data_ptr() for t in co], out.data_ptr(), C, dt, _s())
+    torch.cuda.synchronize()
+    want = ref.bfloat16() if dt & 2 else ref
+    assert torch.equal(out, want)
