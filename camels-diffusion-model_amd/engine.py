@@ -123,13 +123,19 @@ class UNetEngine:
         self.fuse_bn_bwd = self.x16 and os.environ.get("CDM_FUSE_BN_BWD", "1") != "0"
         # a dense BatchNorm + ReLU applied inside the next conv's staging ($CDM_FUSE_BN_FWD=0: apply kernel)
         self.fuse_bn_fwd = self.x16 and os.environ.get("CDM_FUSE_BN_FWD", "1") != "0"
+        # a fused layer's dgrad also stores the dy its staging computes (the BN backward of g), and the weight gradient
+        # stages that dy instead of evaluating the BN backward again in each of its 3 kernel-row blocks
+        # ($CDM_DY_STORE=0 / 1; same-box A/B, 2 runs each: C4 29.64-29.89 -> 29.02-29.04 ms per step, C2 50.57-50.62 ->
+        # 50.36-50.37 ms, profiles/r4_ab_dy_store_ks4.txt)
+        self.dy_store = self.x16 and os.environ.get("CDM_DY_STORE", "1") == "1"
         # a fused producer's BN-backward channel sums accumulated in its consumer's weight-gradient X staging (which
         # stages the producer's y anyway), after the consumer's dgrad wrote the producer's g: no separate pass over g and
-        # y.  On by default for bf16 only: same-box A/B (profiles/r3_ab_bn_sums.txt) C4 33.50 -> 33.29 ms per step, but
-        # C2 (h3) 52.56 -> 55.07 ms — the h3 weight gradient sits at the 256-VGPR limit of 2 waves / SIMD and the sums'
-        # state costs it more than the cdm_norm_bwd_reduce pass it saves.  $CDM_FUSE_BN_SUMS=0 / 1 forces it.
+        # y.  Round 3 kept it off for h3 (C2 52.56 -> 55.07 ms: the h3 weight gradient with the BN-backward dy staging sat
+        # at the 256-VGPR limit); since round 4 the weight gradient stages the dy the dgrad stored (dy_store) and the
+        # sums fit (250 VGPRs, no spill): same-box A/B, 2 runs each, C2 50.36-50.38 -> 49.39-49.45 ms per step
+        # (profiles/r4_ab_sums_dy_pass.txt).  $CDM_FUSE_BN_SUMS=0 / 1 forces it.
         env = os.environ.get("CDM_FUSE_BN_SUMS")
-        self.fuse_bn_sums = self.x16 and (env == "1" if env is not None else not self.h3)
+        self.fuse_bn_sums = self.x16 and (env == "1" if env is not None else (self.dy_store or not self.h3))
         # init_conv.conv1's BN backward inside its weight-gradient kernel ($CDM_FUSE_CIN1_BWD=0: the apply kernel)
         self.fuse_cin1_bwd = os.environ.get("CDM_FUSE_CIN1_BWD", "1") != "0"
         # C4 mixed precision (bf16 arithmetic, train mode): the fused Conv -> BN -> ReLU chain's pre-norm outputs y and
@@ -138,15 +144,12 @@ class UNetEngine:
         # (concatenation slices, pool / FiLM / residual outputs, the C_in = 1 init conv) stay fp32.
         # $CDM_ACT16=0 keeps fp32 activations (A/B checks).
         self.act16 = self.nterm == 1 and os.environ.get("CDM_ACT16", "1") != "0"
-        # a fused layer's dgrad also stores the dy its staging computes (the BN backward of g), and the weight gradient
-        # stages that dy instead of evaluating the BN backward again in each of its 3 kernel-row blocks
-        # ($CDM_DY_STORE=0 / 1; same-box A/B, 2 runs each: C4 29.64-29.89 -> 29.02-29.04 ms per step, C2 50.57-50.62 ->
-        # 50.36-50.37 ms, profiles/r4_ab_dy_store_ks4.txt)
-        self.dy_store = self.x16 and os.environ.get("CDM_DY_STORE", "1") == "1"
         # bf16 (one-term) arithmetic: dy of a fused layer by a separate elementwise pass (cdm_bn_bwd_dy) and the
-        # dgrad on the plain staging schedule instead of the BN-backward staging ($CDM_DY_PASS=0 / 1; same-box A/B,
-        # 2 runs each: C4 36.72-36.96 -> 34.69-34.70 ms per step, profiles/r4_ab_dy_pass_gn_out.txt)
-        self.dy_pass = self.dy_store and self.nterm == 1 and os.environ.get("CDM_DY_PASS", "1") == "1"
+        # dgrad on the plain staging schedule instead of the BN-backward staging ($CDM_DY_PASS=1; off: same-box A/B,
+        # 2 runs each, C4 28.20 -> 28.31-28.33 ms per step — the pass costs 213 us per 64^2 layer, more than the dgrad
+        # gains, profiles/r4_ab_sums_dy_pass.txt; the 36.7 -> 34.7 ms of profiles/r4_ab_dy_pass_gn_out.txt was measured
+        # on a build whose conv epilogue spilled)
+        self.dy_pass = self.dy_store and self.nterm == 1 and os.environ.get("CDM_DY_PASS", "0") == "1"
         # train: out.1's GroupNorm + ReLU inside out.3's forward and weight-gradient staging, zO never written
         # ($CDM_FUSE_GN_OUT=0: the apply kernel writes zO)
         self.fuse_gn_out = os.environ.get("CDM_FUSE_GN_OUT", "1") != "0"

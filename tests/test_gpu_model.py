@@ -304,7 +304,7 @@ def test_fused_bn_fwd_bit_exact_nf128(B):
 @pytest.mark.parametrize("math", ["h3", "bf16"])
 def test_bn_sums_in_consumer_wgrad_nf128(math):
     """The BatchNorm-backward channel sums of each fused dense producer computed in its consumer's weight-gradient X
-    staging (PreBnReluSums, one partial per block; the bf16 default, on demand under h3) vs the separate
+    staging (PreBnReluSums, one partial per block; the default since round 4) vs the separate
     cdm_norm_bwd_reduce pass, n_feat
     128, B=3: the forward (eps, running statistics) is untouched (bit-identical); the gradients differ only by the sums'
     fp32 summation order, which moves the BN-backward coefficients by rounding: relative L2 per gradient <= 1e-2 (the
