@@ -14,7 +14,10 @@ kernels the engine uses for the same layers: BatchNorm / ReLU / MaxPool backward
 (`cdm_norm_bwd_reduce`, `cdm_bn_bwd_finalize`, `cdm_norm_apply_bwd`), conv weight gradients (`cdm_conv3x3_wgrad`, the
 C_in = 1 form `cdm_conv3x3_cin1_wgrad`), input gradients (the conv on the flipped weights), ConvTranspose backward
 (`cdm_convT2x2_wgrad / dgrad`), EmbedFC backward (`cdm_embed_bwd`).  Parameter gradients always; the input gradient
-where the input has C_in > 1 channels (EmbedFC: input_dim % 4 == 0).  Eval-mode backward raises, as ContextUnet's.
+of every input (EmbedFC: input_dim % 4 == 0), incl. the C_in = 1 image of a ResidualConvBlock(1, C) (the flipped-weight
+conv `cdm_conv3x3_cin1_dgrad`, plus the random 1x1 shortcut's sum_c w[c] g[c] for is_res).  Eval-mode calls under
+autograd run the same taped form with BatchNorm frozen on the running statistics (`cdm_bn_fwd_frozen`, backward
+`cdm_bn_bwd_finalize_frozen`: the backward of batch_norm(training=False)), as ContextUnet's.
 """
 from __future__ import annotations
 
@@ -36,23 +39,11 @@ def _s() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
-class _BlockNoBackward(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, out, *params):
-        return out.view_as(out)
-
-    @staticmethod
-    def backward(ctx, *grads):
-        raise NotImplementedError("a backward through an eval-mode (running-statistics) BatchNorm block is not built on "
-                                  "the HIP path, as for ContextUnet; run the block in train mode")
-
-
 def _finish(out: torch.Tensor, module: nn.Module, tape=None, inputs=()) -> torch.Tensor:
     params = [p for p in module.parameters() if p.requires_grad]
     if torch.is_grad_enabled() and (params or any(x.requires_grad for x in inputs)):
-        if tape is not None:
-            return _BlockFunction.apply(tape, out, len(inputs), *inputs, *params)
-        return _BlockNoBackward.apply(out, *params)
+        assert tape is not None, "a differentiable block call records a tape"
+        return _BlockFunction.apply(tape, out, len(inputs), *inputs, *params)
     return out
 
 
@@ -70,6 +61,8 @@ class _Tape:
         self.grads = {}
         self.first_rec = None      # the block's first conv layer: its input gradient only when the input needs one
         self.need_input = True
+        self.resid_g = None        # C_in = 1 is_res block: the block-output gradient and the shortcut weights, for the
+        self.resid_w = None        # image gradient (sum_c w[c] g[c]) added by the first layer's backward
 
     def need_dx(self, rec) -> bool:
         return rec is not self.first_rec or self.need_input
@@ -130,9 +123,11 @@ def _layer_backward(rec, tape: _Tape, g: torch.Tensor, need_dx: bool):
     ws = _dpart(dev)
     nparts = fold(ws, slab.data_ptr(), B * nch, 5, Cout, s)
     dgamma, dbeta, A, Bc, Cc, dbias = [E(Cout) for _ in range(6)]
-    L.cdm_bn_bwd_finalize(ws.dpart.data_ptr(), nparts, Cout, float(P), bn.weight.data_ptr(), invstd.data_ptr(),
-                          dgamma.data_ptr(), dbeta.data_ptr(), A.data_ptr(), Bc.data_ptr(), Cc.data_ptr(),
-                          dbias.data_ptr(), s)
+    fin = L.cdm_bn_bwd_finalize_frozen if rec["frozen"] else L.cdm_bn_bwd_finalize
+    fin(ws.dpart.data_ptr(), nparts, Cout, float(P), bn.weight.data_ptr(), invstd.data_ptr(), dgamma.data_ptr(),
+        dbeta.data_ptr(), A.data_ptr(), Bc.data_ptr(), Cc.data_ptr(), dbias.data_ptr(), s)
+    if rec.get("resid_w") is not None:       # this layer's apply added the C_in = 1 shortcut: keep g for the image grad
+        tape.resid_g, tape.resid_w = g, rec["resid_w"]
     dy = E(P, Cout)
     L.cdm_norm_apply_bwd(mode, g.data_ptr(), Cout, y.data_ptr(), Cout, B, H, W, Cout, scale.data_ptr(), shift.data_ptr(),
                          0, mean.data_ptr(), invstd.data_ptr(), 0, 1, None, 0, A.data_ptr(), Bc.data_ptr(), Cc.data_ptr(),
@@ -155,8 +150,12 @@ def _layer_backward(rec, tape: _Tape, g: torch.Tensor, need_dx: bool):
         L.cdm_conv3x3_cin1_wgrad(dy.data_ptr(), Cout, xh.data_ptr(), B, H, W, Cout, CHUNK, slw.data_ptr(), s)
         nparts = fold(ws, slw.data_ptr(), nt, 10, Cout, s)
         L.cdm_slab_sum_all(ws.dpart.data_ptr(), nparts, 10, 0, 9, Cout, dW.data_ptr(), 1, 9, 0, s)
-        if need_dx:
-            raise NotImplementedError("the input gradient of a C_in = 1 block (the image) is not built on the HIP path")
+        if need_dx:   # the image: the tap-flipped conv over dy, plus the shortcut's sum_c w[c] g_out[c] (is_res)
+            dx = E(P)
+            gres, sw = tape.resid_g, tape.resid_w
+            L.cdm_conv3x3_cin1_dgrad(dy.data_ptr(), Cout, None, 0, None, None, None, None, None, None, None,
+                                     conv.weight.detach().contiguous().data_ptr(), _p(gres), Cout if gres is not None else 0,
+                                     _p(sw), B, B, H, W, Cout, dx.data_ptr(), s)
     tape.add(conv.weight, dW)
     tape.add(conv.bias, dbias)
     tape.add(bn.weight, dgamma)
@@ -199,7 +198,8 @@ def conv_bn_relu(seq: nn.Sequential, xh: torch.Tensor, B: int, H: int, W: int, p
     kc = conv_kc(Cin, Cout)
     E = lambda *shape: torch.empty(*shape, device=dev)   # noqa: E731
     Wt, bt = conv.weight.detach().contiguous(), conv.bias.detach().contiguous()
-    if bn.training:
+    frozen = not bn.training          # eval mode: only reaches the taped form when the call is differentiable
+    if bn.training or tape is not None:
         wpk = E(9 * Cin, Cout)
         L.cdm_pack_conv3x3(Wt.data_ptr(), bt.data_ptr(), Cin, Cout, None, None, None, None, 0.0, wpk.data_ptr(), None,
                            None, kc, s)
@@ -220,10 +220,14 @@ def conv_bn_relu(seq: nn.Sequential, xh: torch.Tensor, B: int, H: int, W: int, p
         st = [E(Cout) for _ in range(4)]                  # mean, invstd, scale, shift
         track = bn.track_running_stats and bn.running_mean is not None
         mom = 0.1 if bn.momentum is None else float(bn.momentum)
-        L.cdm_bn_fwd_finalize(ws.dpart.data_ptr(), nparts, 2, Cout, float(P), bn.weight.data_ptr(), bn.bias.data_ptr(),
-                              _p(bn.running_mean) if track else None, _p(bn.running_var) if track else None,
-                              _p(bn.num_batches_tracked) if track else None, mom, float(bn.eps),
-                              *[t.data_ptr() for t in st], None, 0, None, s)
+        if frozen:                                        # running statistics, not updated
+            L.cdm_bn_fwd_frozen(Cout, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
+                                bn.running_var.data_ptr(), float(bn.eps), *[t.data_ptr() for t in st], None, 0, None, s)
+        else:
+            L.cdm_bn_fwd_finalize(ws.dpart.data_ptr(), nparts, 2, Cout, float(P), bn.weight.data_ptr(),
+                                  bn.bias.data_ptr(), _p(bn.running_mean) if track else None,
+                                  _p(bn.running_var) if track else None, _p(bn.num_batches_tracked) if track else None,
+                                  mom, float(bn.eps), *[t.data_ptr() for t in st], None, 0, None, s)
         scale, shift, flags = st[2], st[3], APPLY_RELU
         if tape is not None:
             wdg = None
@@ -232,7 +236,8 @@ def conv_bn_relu(seq: nn.Sequential, xh: torch.Tensor, B: int, H: int, W: int, p
                 L.cdm_pack_conv3x3(Wt.data_ptr(), bt.data_ptr(), Cin, Cout, None, None, None, None, 0.0,
                                    E(9 * Cin, Cout).data_ptr(), None, wdg.data_ptr(), kc, s)
             # (C_in = 1: the NHWC input [B*H*W, 1] is the NCHW map the C_in = 1 weight gradient reads)
-            rec = dict(dims=(B, H, W, Cin, Cout), conv=conv, bn=bn, st=st, y=y, pool=pool, wdg=wdg, kc=kc, x=xh)
+            rec = dict(dims=(B, H, W, Cin, Cout), conv=conv, bn=bn, st=st, y=y, pool=pool, wdg=wdg, kc=kc, x=xh,
+                       frozen=frozen, resid_w=None if resid is None else resid[1])
             if not tape.ops:
                 tape.first_rec = rec
             tape.ops.append(lambda g, rec=rec: _layer_backward(rec, tape, g, tape.need_dx(rec)))
@@ -320,8 +325,9 @@ def residual_block(blk, xh: torch.Tensor, x_nchw: torch.Tensor, B: int, H: int, 
 
 
 def _new_tape(module: nn.Module, *inputs):
-    """A tape when this call must be differentiable (train mode, grad enabled, something requires grad), else None."""
-    if not (torch.is_grad_enabled() and module.training):
+    """A tape when this call must be differentiable (grad enabled, something requires grad), else None.  Eval mode
+    records the same tape with BatchNorm frozen on the running statistics."""
+    if not torch.is_grad_enabled():
         return None
     if not (any(p.requires_grad for p in module.parameters()) or any(x.requires_grad for x in inputs)):
         return None

@@ -749,10 +749,10 @@ __global__ __launch_bounds__(256) void embed_bwd_act_kernel(Mlp4 P) {
 
 // parameter grads (assign): dw2[j][i], db2[j], dw1[i][k], db1[i]; each a sequential fp64 sum over the rows (the
 // product of two fp32 values is exact in fp64, so fma and multiply-add give the same bits).  dw2 (E x E outputs, the
-// bulk) in 64 x 64 tiles: the block stages 64 rows of dout and h through LDS and each thread carries 4 x 4 outputs, 16
-// independent fp64 chains (the per-output form waited on one global load per row: 40 us per C2 step, latency-bound);
-// blocks past the tiles take db2, dw1, db1 one output per thread.
-constexpr int EMB_T = 64;
+// bulk) in 32 x 32 tiles (160 blocks for the four MLPs at n_feat 128): the block stages 64 rows of dout and h through
+// LDS and each thread carries 2 x 2 outputs (the per-output form waited on one global load per row: 40 us per C2 step,
+// latency-bound; 64 x 64 tiles ran 40 blocks, 30 us); blocks past the tiles take db2, dw1, db1 one output per thread.
+constexpr int EMB_T = 32, EMB_R = 64;
 static __host__ __device__ inline int embed_tiles(int E) { return ((E + EMB_T - 1) / EMB_T) * ((E + EMB_T - 1) / EMB_T); }
 __global__ __launch_bounds__(256) void embed_bwd_param_kernel(Mlp4 P) {
     const MlpDesc& d = P.m[blockIdx.y];
@@ -760,48 +760,45 @@ __global__ __launch_bounds__(256) void embed_bwd_param_kernel(Mlp4 P) {
     const int nt = embed_tiles(E);
     const int tid = threadIdx.x;
     if ((int)blockIdx.x < nt) {
-        __shared__ __attribute__((aligned(16))) float ds_[EMB_T][EMB_T], hs_[EMB_T][EMB_T];
+        __shared__ __attribute__((aligned(16))) float ds_[EMB_R][EMB_T], hs_[EMB_R][EMB_T];
         const int tpr = (E + EMB_T - 1) / EMB_T;
         const int j0 = (blockIdx.x / tpr) * EMB_T, i0 = (blockIdx.x % tpr) * EMB_T;
-        const int tj = (tid >> 4) * 4, ti = (tid & 15) * 4;
-        double s[4][4];
+        const int tj = (tid >> 4) * 2, ti = (tid & 15) * 2;
+        double s[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+        constexpr int PER = EMB_R * EMB_T / 256;
+        for (int b0 = 0; b0 < rows; b0 += EMB_R) {
+            const int nb = min(EMB_R, rows - b0);
+            // the chunk's 2 x PER loads per thread issued together (then stored): one memory latency per chunk
+            float dv_[PER], hv_[PER];
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) s[a][c] = 0.0;
-        for (int b0 = 0; b0 < rows; b0 += EMB_T) {
-            const int nb = min(EMB_T, rows - b0);
-            // the chunk's 2 x 16 loads per thread issued together (then stored): one memory latency per chunk
-            float dv_[EMB_T * EMB_T / 256], hv_[EMB_T * EMB_T / 256];
-#pragma unroll
-            for (int u = 0; u < EMB_T * EMB_T / 256; ++u) {
+            for (int u = 0; u < PER; ++u) {
                 const int q = tid + u * 256, r = q / EMB_T, c = q - r * EMB_T;
                 const bool ok = r < nb;
                 dv_[u] = ok && j0 + c < E ? d.dout[(long long)(b0 + r) * E + j0 + c] : 0.f;
                 hv_[u] = ok && i0 + c < E ? d.h[(long long)(b0 + r) * E + i0 + c] : 0.f;
             }
 #pragma unroll
-            for (int u = 0; u < EMB_T * EMB_T / 256; ++u) {
+            for (int u = 0; u < PER; ++u) {
                 const int q = tid + u * 256, r = q / EMB_T, c = q - r * EMB_T;
                 ds_[r][c] = dv_[u];
                 hs_[r][c] = hv_[u];
             }
             __syncthreads();
             for (int r = 0; r < nb; ++r) {
-                const float4 dv = *reinterpret_cast<const float4*>(&ds_[r][tj]);
-                const float4 hv = *reinterpret_cast<const float4*>(&hs_[r][ti]);
-                const double dd[4] = {dv.x, dv.y, dv.z, dv.w}, hh[4] = {hv.x, hv.y, hv.z, hv.w};
+                const float2 dv = *reinterpret_cast<const float2*>(&ds_[r][tj]);
+                const float2 hv = *reinterpret_cast<const float2*>(&hs_[r][ti]);
+                const double dd[2] = {dv.x, dv.y}, hh[2] = {hv.x, hv.y};
 #pragma unroll
-                for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < 2; ++a)
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) s[a][c] = fma(dd[a], hh[c], s[a][c]);
+                    for (int c = 0; c < 2; ++c) s[a][c] = fma(dd[a], hh[c], s[a][c]);
             }
             __syncthreads();
         }
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
+            for (int c = 0; c < 2; ++c) {
                 const int j = j0 + tj + a, i = i0 + ti + c;
                 if (j < E && i < E) d.dw2[(long long)j * E + i] = (float)s[a][c];
             }

@@ -154,8 +154,30 @@ def test_residual_block_is_res_backward_params():
             continue
         e = ((p.grad.cpu() - refp[n].grad).norm() / refp[n].grad.norm()).item()
         assert e < 1e-4, (n, e)
-    with pytest.raises(NotImplementedError):
-        gpu(x.cuda().requires_grad_(True)).sum().backward()
+
+
+@pytest.mark.parametrize("is_res", [True, False])
+def test_residual_block_cin1_image_grad(is_res):
+    """The image gradient of a C_in = 1 block (ContextUnet's init_conv form): the tap-flipped conv over conv1's BN
+    backward plus, for is_res, the fresh 1x1 shortcut's sum_c w[c] g[c]; vs torch autograd on the CPU."""
+    from cdm_amd import ResidualConvBlock
+    torch.manual_seed(3)
+    cpu = ResidualConvBlock(1, 32, is_res=is_res)
+    gpu = copy.deepcopy(cpu).cuda()
+    g_ = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 1, 16, 16, generator=g_)
+    w = torch.randn(2, 32, 16, 16, generator=g_)
+    xc = x.clone().requires_grad_(True)
+    torch.manual_seed(7)
+    ref = (torch.nn.Conv2d(1, 32, 1)(xc) + _rcb_ref(cpu, xc)) if is_res else _rcb_ref(cpu, xc)
+    (ref * w).sum().backward()
+    xg = x.cuda().requires_grad_(True)
+    torch.manual_seed(7)
+    got = gpu(xg)
+    assert _rel(got, ref) < 1e-4
+    (got * w.cuda()).sum().backward()
+    e = ((xg.grad.cpu() - xc.grad).norm() / xc.grad.norm()).item()
+    assert e < 1e-4, e
 
 
 def test_unet_down_up_backward():
@@ -188,12 +210,50 @@ def test_embed_fc_backward(in_dim):
             assert ((p.grad.cpu() - r.grad).norm() / r.grad.norm()).item() < 1e-5, n
 
 
-def test_eval_block_backward_raises():
-    from cdm_amd import ResidualConvBlock
-    gpu = ResidualConvBlock(16, 32).cuda().eval()
-    out = gpu(torch.randn(2, 16, 8, 8, device="cuda"))
-    with pytest.raises(NotImplementedError):
-        out.sum().backward()
+@pytest.mark.parametrize("kind", ["rcb", "down", "cin1_res"])
+def test_eval_block_backward(kind):
+    """Gradients through an eval-mode block (BatchNorm on the running statistics, batch_norm(training=False) under
+    autograd: the conv biases get a gradient here), parameters and input, vs torch autograd of the same modules in eval
+    mode on the CPU; running statistics untouched."""
+    from cdm_amd import ResidualConvBlock, UnetDown
+    torch.manual_seed(17)
+    if kind == "rcb":
+        cpu, shape = ResidualConvBlock(16, 32), (2, 16, 8, 8)
+        ref_fn = lambda v: _rcb_ref(cpu, v)   # noqa: E731
+    elif kind == "down":
+        cpu, shape = UnetDown(16, 32), (2, 16, 16, 16)
+        ref_fn = lambda v: F.max_pool2d(_rcb_ref(cpu.model[1], _rcb_ref(cpu.model[0], v)), 2)   # noqa: E731
+    else:
+        cpu, shape = ResidualConvBlock(1, 32, is_res=True), (2, 1, 16, 16)
+        ref_fn = lambda v: torch.nn.Conv2d(1, 32, 1)(v) + _rcb_ref(cpu, v)   # noqa: E731
+    for m in cpu.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.2, 0.2); m.running_var.uniform_(0.5, 1.5)
+    cpu.eval()
+    gpu = copy.deepcopy(cpu).cuda().eval()
+    run0 = {k: v.clone() for k, v in gpu.state_dict().items()}
+    g_ = torch.Generator().manual_seed(18)
+    x = torch.randn(*shape, generator=g_)
+    xc = x.clone().requires_grad_(True)
+    torch.manual_seed(7)
+    ref = ref_fn(xc)
+    w = torch.randn(ref.shape, generator=g_)
+    (ref * w).sum().backward()
+    xg = x.cuda().requires_grad_(True)
+    torch.manual_seed(7)
+    got = gpu(xg)
+    assert _rel(got, ref) < 1e-4
+    (got * w.cuda()).sum().backward()
+    refp = dict(cpu.named_parameters())
+    for n, p in gpu.named_parameters():
+        r = refp[n].grad
+        assert p.grad is not None, n
+        e = ((p.grad.cpu() - r).norm() / r.norm()).item()
+        assert e < 1e-4, (n, e)
+    e = ((xg.grad.cpu() - xc.grad).norm() / xc.grad.norm()).item()
+    assert e < 1e-4, e
+    for k, v in gpu.state_dict().items():
+        assert torch.equal(v, run0[k]), k
 
 
 @pytest.mark.parametrize("cin,cout", [(32, 32), (16, 32)])
