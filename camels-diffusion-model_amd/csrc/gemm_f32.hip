@@ -804,9 +804,12 @@ __global__ __launch_bounds__(GTHREADS, MINB) void gemm_x3_kernel(SA sa0, SB sb0,
     e(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
 }
 
-static int gemm_minb() {    // $CDM_GEMM_MINB: 4 (the default) or 2 resident blocks per CU asked of the compiler
-    static const int v = [] { const char* e = getenv("CDM_GEMM_MINB"); return e ? atoi(e) : 4; }();
-    return v;
+// $CDM_GEMM_MINB: 4 or 2 resident blocks per CU asked of the compiler; default 4 for h3 (profiles/r3_ab_gemm_minb.txt),
+// 2 for the one-term bf16 arithmetic, whose 4-block form spills 51 VGPRs (with the bf16 knobs below, same-box A/B:
+// C4 27.95-28.02 -> 27.73-27.75 ms per step, profiles/r4_ab_c4_knobs.txt)
+static int gemm_minb(int nterm) {
+    static const int v = [] { const char* e = getenv("CDM_GEMM_MINB"); return e ? atoi(e) : 0; }();
+    return v > 0 ? v : (nterm == 1 ? 2 : 4);
 }
 
 static int gemm_order() {   // $CDM_GEMM_ORDER: 1 operand-sharing block order (default), 0 grid order
@@ -827,7 +830,7 @@ static int launch_gemm_x3(MkA mka, MkB mkb, const EP& ep, int M, int N, int K, i
     const int order = gemm_order();
     switch (nterm) {
         case 1:
-            if (gemm_minb() == 4)
+            if (gemm_minb(1) == 4)
                 hipLaunchKernelGGL((gemm_x3_kernel<SAT<1>, SBT<1>, EP, 1, XCD_REMAP, 1, 4>), grid, dim3(GTHREADS), 0, s,
                                    mka.template make<1>(), mkb.template make<1>(), ep, K, per, order);
             else
@@ -837,7 +840,7 @@ static int launch_gemm_x3(MkA mka, MkB mkb, const EP& ep, int M, int N, int K, i
         case 3: hipLaunchKernelGGL((gemm_x3_kernel<SAT<3>, SBT<3>, EP, 3, XCD_REMAP>), grid, dim3(GTHREADS), 0, s,
                                    mka.template make<3>(), mkb.template make<3>(), ep, K, per, order); break;
         case NT_H3:
-            if (gemm_minb() == 4)
+            if (gemm_minb(NT_H3) == 4)
                 hipLaunchKernelGGL((gemm_x3_kernel<SAT<NT_H3>, SBT<NT_H3>, EP, NT_H3, XCD_REMAP, 1, 4>), grid,
                                    dim3(GTHREADS), 0, s, mka.template make<NT_H3>(), mkb.template make<NT_H3>(), ep, K,
                                    per, order);
@@ -1902,9 +1905,9 @@ static int halo_tpb(int mtiles, int ntiles, int nterm, int wt) {
 // the staggered halo split of the LDS-halo conv: on for h3, off for the one-term bf16 images ($CDM_HALO_STAGGER=0 / 1
 // forces it).  Same-box A/B, 2 rounds (profiles/r3_ab_halo_stagger.txt): C2 (h3) train step 51.92-51.95 -> 51.34-51.44
 // ms; C4 (bf16) 32.20-32.21 -> 32.26-32.40 ms (its halo split is a plain conversion: nothing left to hide)
-static int halo_stagger(int nterm) {
+static int halo_stagger(int nterm) {   // default on for h3 and (round 4, profiles/r4_ab_c4_knobs.txt) for bf16
     static const int v = [] { const char* e = getenv("CDM_HALO_STAGGER"); return e ? atoi(e) : -1; }();
-    return v >= 0 ? v : (nterm == NT_H3 ? 1 : 0);
+    return v >= 0 ? v : ((nterm == NT_H3 || nterm == 1) ? 1 : 0);
 }
 
 // the one-barrier-per-chunk schedule of the one-term (bf16) LDS-halo conv ($CDM_HALO_ONEB=0: three barriers per chunk)
@@ -1913,8 +1916,9 @@ static int halo_oneb() {
     return v;
 }
 
-static int halo_oneb_bwd() {
-    static const int v = [] { const char* e = getenv("CDM_HALO_ONEB_BWD"); return e ? atoi(e) : 0; }();
+static int halo_oneb_bwd() {   // the bf16 BN-backward dgrad, one barrier per chunk: default on since round 4 (bf16
+                               // g / y; profiles/r4_ab_c4_knobs.txt)
+    static const int v = [] { const char* e = getenv("CDM_HALO_ONEB_BWD"); return e ? atoi(e) : 1; }();
     return v;
 }
 

@@ -389,14 +389,16 @@ __global__ __launch_bounds__(256) void conv_cin1_dgrad_kernel(const float* g1, i
 // HPM: halo pixels the LDS images hold, (R + 2) W rounded up to 64: 384 for W <= 64 (40 KiB of LDS, 4 blocks per CU;
 // the W-independent 768-pixel images took 80 KiB, 2 blocks per CU, half the loads in flight: 2.3 TB/s), 512 for W = 128,
 // 768 for W = 256
+// HPM threads per block, one halo pixel each in the tap reduction (256 threads over 384 halo pixels left half the
+// waves with a second pixel: the SIMDs holding waves 0-1 did twice the FMAs of the others)
 template <int HPM>
-__global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* __restrict__ z, int ldz, int H, int W,
+__global__ __launch_bounds__(HPM) void conv_cout1_fwd_band_kernel(const float* __restrict__ z, int ldz, int H, int W,
                                                                   int C, const float* __restrict__ w,
                                                                   const float* __restrict__ bias,
                                                                   float* __restrict__ out,
                                                                   const float* __restrict__ gs,
                                                                   const float* __restrict__ gt) {
-    constexpr int KQ = (HPM + 255) / 256;             // halo pixels per thread in the tap reduction
+    constexpr int KQ = 1;                             // halo pixels per thread in the tap reduction
     __shared__ float zt[HPM * 17];                    // [halo px][16 ch + 1 pad]
     __shared__ float st[9 * HPM];                     // [tap][halo px]
     const int R = 256 / W, HP = (R + 2) * W;
@@ -412,11 +414,11 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* _
         for (int t = 0; t < 9; ++t) acc[k][t] = 0.f;
     // staging: piece i of this thread = (halo pixel q4>>2, channels 4(q4&3)..+3) of the current 16-channel slab;
     // the next slab's pieces are loaded into registers while this slab is reduced (one slab of latency hidden)
-    constexpr int PQ = HPM * 4 / 256;
+    constexpr int PQ = 4;                             // HPM * 4 pieces over HPM threads
     const float* src[PQ];
 #pragma unroll
     for (int i = 0; i < PQ; ++i) {
-        const int q4 = tid + i * 256, q = q4 >> 2, part = q4 & 3;
+        const int q4 = tid + i * HPM, q = q4 >> 2, part = q4 & 3;
         const int hh = h0 - 1 + q / W, ww = q - (q / W) * W;
         src[i] = (q < HP && (unsigned)hh < (unsigned)H) ? z + (((long long)n * H + hh) * W + ww) * ldz + part * 4
                                                         : nullptr;
@@ -436,7 +438,7 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* _
         }
 #pragma unroll
         for (int i = 0; i < PQ; ++i) {
-            const int q4 = tid + i * 256;
+            const int q4 = tid + i * HPM;
             if ((q4 >> 2) < HP) {
                 float v[4] = {pre[i].x, pre[i].y, pre[i].z, pre[i].w};
                 if (gs && src[i]) {
@@ -451,7 +453,7 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* _
         if (c0 + 16 < C) gload(c0 + 16);
 #pragma unroll
         for (int k = 0; k < KQ; ++k) {
-            const int q = tid + k * 256;
+            const int q = tid + k * HPM;
             if (q < HP) {
 #pragma unroll
                 for (int c = 0; c < 16; ++c) {
@@ -465,7 +467,7 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* _
     }
 #pragma unroll
     for (int k = 0; k < KQ; ++k) {
-        const int q = tid + k * 256;
+        const int q = tid + k * HPM;
         if (q < HP) {
 #pragma unroll
             for (int t = 0; t < 9; ++t) st[t * HP + q] = acc[k][t];
@@ -473,6 +475,7 @@ __global__ __launch_bounds__(256) void conv_cout1_fwd_band_kernel(const float* _
     }
     __syncthreads();
     // output pixel (h0 + r, c): sum over taps of the partial of halo pixel (r + ky, c + kx - 1)
+    if (tid >= 256) return;
     const int r = tid / W, c = tid - r * W;
     float o = bias[0];
 #pragma unroll
@@ -1140,11 +1143,11 @@ static int launch_cout1_band(const float* z, int ldz, int N, int H, int W, int C
     const dim3 grid(N * (H / (256 / W)));
     const int hp = (256 / W + 2) * W;           // halo pixels of a band
     if (hp <= 384)
-        hipLaunchKernelGGL(conv_cout1_fwd_band_kernel<384>, grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
+        hipLaunchKernelGGL(conv_cout1_fwd_band_kernel<384>, grid, dim3(384), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
     else if (hp <= 512)
-        hipLaunchKernelGGL(conv_cout1_fwd_band_kernel<512>, grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
+        hipLaunchKernelGGL(conv_cout1_fwd_band_kernel<512>, grid, dim3(512), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
     else
-        hipLaunchKernelGGL(conv_cout1_fwd_band_kernel<768>, grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
+        hipLaunchKernelGGL(conv_cout1_fwd_band_kernel<768>, grid, dim3(768), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
     return cdm_status();
 }
 CDM_API int cdm_conv3x3_cout1_fwd(const float* z, int ldz, int N, int H, int W, int C, const float* w, const float* bias,
