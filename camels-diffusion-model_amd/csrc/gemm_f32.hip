@@ -164,8 +164,9 @@ struct LdConvT2x2GatherB {  // convT 2x2 wgrad: B(k = input pix (n,h,w), n = ij*
 // ============================== epilogues ==============================
 // Accumulator element (i, j, r) of a wave sits at row  mw + 32i + (r&3) + 8(r>>2) + 4(lane>>5)
 //                                             column nw + 32j + (lane&31).
-#define CDM_FOR_ACC(...)                                                                   \
-    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                           \
+#define CDM_FOR_ACC(...) CDM_FOR_ACC_N(2, __VA_ARGS__)
+#define CDM_FOR_ACC_N(NI, ...)                                                             \
+    _Pragma("unroll") for (int i = 0; i < NI; ++i)                                          \
     _Pragma("unroll") for (int j = 0; j < 2; ++j)                                           \
     _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                        \
         const int m = mw + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);              \
@@ -303,6 +304,123 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
                 for (int w = 1; w < WM; ++w) {
                     mx = fmaxf(mx, scratch[w * GBN + tid]);
                     mn = fminf(mn, scratch[(WM + w) * GBN + tid]);
+                }
+                atomicMax(ymm + n, fkey(mx));
+                atomicMin(ymm + ymm_ld + n, fkey(mn));
+            }
+        }
+    }
+
+    // tall wave tiles (conv3x3_halo_x3_kernel, ABL 8192; 2 waves along M of the 256-row block): the wave holds rows
+    // mw..mw+127 (4 row blocks of 32) x columns nw..nw+63, i.e. exactly one 128-row stats tile, written directly
+    __device__ __forceinline__ void tall(f32x16 (&acc)[4][2], int mw, int nw, int lane, int wm, int wn, float* scratch,
+                                         int tid) const {
+        static_assert(WM == 4, "tall tiles: a 256-row block");
+        constexpr int NWM = 2;   // waves along M
+        OT* yz = y + (long long)blockIdx.z * zstride;
+        // column sums per half (row blocks 0-1, 2-3), added as the 64 x 64 form adds its two waves: identical stats
+        float cs[2][2] = {{0.f, 0.f}, {0.f, 0.f}}, cq[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+        float cmx[2] = {-INFINITY, -INFINITY}, cmn[2] = {INFINITY, INFINITY};
+        float am = 0.f;
+        const bool relu = flags & EPI_RELU;
+        const bool accum = flags & EPI_ACCUM;
+        if (mw + 128 <= M && (nw - wn * 64) + GBN <= N) {
+            float bj[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bj[j] = bias ? bias[(nw + 32 * j + (lane & 31)) % bias_mod] : 0.f;
+            if constexpr (ACC) {   // the load-ahead accumulate (see operator())
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        float old[16];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = mw + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                            old[r] = Act<OT>::load(yz + (long long)m * ldy + nw + 32 * j + (lane & 31));
+                        }
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = mw + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                            const int n = nw + 32 * j + (lane & 31);
+                            float v = acc[i][j][r] + bj[j] + old[r];
+                            if (relu) v = relu_f(v);
+                            v = Act<OT>::round(v);
+                            Act<OT>::store(yz + (long long)m * ldy + n, v);
+                            cs[i >> 1][j] += v; cq[i >> 1][j] += v * v;
+                            am = fmaxf(am, fabsf(v));
+                            cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
+                        }
+                    }
+            } else {
+                CDM_FOR_ACC_N(4, {
+                    float v = acc[i][j][r] + bj[j];
+                    if (accum) v += Act<OT>::load(yz + (long long)m * ldy + n);
+                    if (relu) v = relu_f(v);
+                    v = Act<OT>::round(v);
+                    Act<OT>::store(yz + (long long)m * ldy + n, v);
+                    cs[i >> 1][j] += v; cq[i >> 1][j] += v * v;
+                    am = fmaxf(am, fabsf(v));
+                    cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
+                })
+            }
+        } else {
+            CDM_FOR_ACC_N(4, {
+                if (m < M && n < N) {
+                    float v = acc[i][j][r];
+                    if (bias) v += bias[n % bias_mod];
+                    OT* p = yz + (long long)m * ldy + n;
+                    if (accum) v += Act<OT>::load(p);
+                    if (relu) v = relu_f(v);
+                    v = Act<OT>::round(v);
+                    Act<OT>::store(p, v);
+                    cs[i >> 1][j] += v; cq[i >> 1][j] += v * v;
+                    am = fmaxf(am, fabsf(v));
+                    cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
+                }
+            })
+        }
+        if (amax) block_amax_commit(am, amax);
+        if (!stats) return;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                cs[h][j] += __shfl_xor(cs[h][j], 32, 64);
+                cq[h][j] += __shfl_xor(cq[h][j], 32, 64);
+            }
+        if (lane < 32) {
+            float* st = stats + (long long)(mw / GBM) * 2 * stats_ld;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int n = nw + 32 * j + lane;
+                if (n < N) { st[n] = cs[0][j] + cs[1][j]; st[stats_ld + n] = cq[0][j] + cq[1][j]; }
+            }
+        }
+        if (!ymm) return;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            cmx[j] = fmaxf(cmx[j], __shfl_xor(cmx[j], 32, 64));
+            cmn[j] = fminf(cmn[j], __shfl_xor(cmn[j], 32, 64));
+        }
+        __syncthreads();  // scratch aliases the operand LDS
+        if (lane < 32) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int c = wn * 64 + 32 * j + lane;
+                scratch[wm * GBN + c] = cmx[j];
+                scratch[(NWM + wm) * GBN + c] = cmn[j];
+            }
+        }
+        __syncthreads();
+        if (tid < GBN) {
+            const int n = (nw - wn * 64) + tid;
+            if (n < N) {
+                float mx = scratch[tid], mn = scratch[NWM * GBN + tid];
+#pragma unroll
+                for (int w = 1; w < NWM; ++w) {
+                    mx = fmaxf(mx, scratch[w * GBN + tid]);
+                    mn = fminf(mn, scratch[(NWM + w) * GBN + tid]);
                 }
                 atomicMax(ymm + n, fkey(mx));
                 atomicMin(ymm + ymm_ld + n, fkey(mn));
@@ -934,17 +1052,28 @@ constexpr int HTHREADS = 512;
 // priority 1 for waves 4-7
 // XT: element type of the source x (and of PRE's y): bf16 for C4's fused-chain activations / gradients
 template <int NT, int WT, class EP, bool XCD_REMAP, int ABL = (NT >= 6 ? 0 : 1), class PRE = PreNone, class XT = float>
-__global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* __restrict__ x, int H, int Cin,
+__global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* __restrict__ x, int H, int Cin,
                                                                       int ldx, const __bf16* __restrict__ wx3,
                                                                       int Cout, const float* amax_x,
                                                                       const float* amax_w, EP ep, PRE pre,
                                                                       int mtiles, int tpb, int stg = 0) {
     constexpr int NS = XTerms<NT>::NS;
-    constexpr int ROWS = HBM_ / WT, HR = ROWS + 2, HC = WT + 2, HPX = HR * HC;
-    constexpr int HQ = (HPX * 4 + HTHREADS - 1) / HTHREADS;   // float4 halo pieces per thread
+    // TALL (ABL 8192, one bf16 term only): 4 waves (one per SIMD, 512 registers each: the accumulators live in AGPRs) as
+    // 2 (M) x 2 (N) of 128 x 64 — 4 row blocks of 32 pixels per wave.  The one-term MFMA reads 1 KiB of fragments per
+    // 32x32x16 product from LDS at 64 x 64 (the CU's LDS rate at full MFMA rate); 128 x 64 reads 0.75 KiB.  Same
+    // 256-pixel x 128-channel block tile and LDS images as the 8-wave form; launched with 256 threads.  Measured (round
+    // 4, profiles/r4_ab_halo_tall.txt): bit-identical C4 train steps, but 29.3 vs 27.5 ms — one wave per SIMD leaves
+    // the staging and barrier waits uncovered (forward 64^2 414 vs 326 us).  Kept as an ablation bit, not dispatched.
+    constexpr bool TALL = (ABL & 8192) != 0;
+    static_assert(!TALL || NS == 1, "tall wave tiles: the one-term images only");
+    constexpr int MI = TALL ? 4 : 2;                  // 32-row blocks per wave
+    constexpr int NTH = TALL ? 256 : HTHREADS;        // threads per block
+    constexpr int HB = HBM_;                          // output pixels per tile
+    constexpr int ROWS = HB / WT, HR = ROWS + 2, HC = WT + 2, HPX = HR * HC;
+    constexpr int HQ = (HPX * 4 + NTH - 1) / NTH;   // float4 halo pieces per thread
     // halo planes padded to HQ x 512 pieces where LDS allows: every piece then has a slot (past-the-halo pieces
     // write unused padding), so the split + store has no branches and can share a scheduling region with MFMAs
-    constexpr int HPXA = HQ * HTHREADS / 4;
+    constexpr int HPXA = HQ * NTH / 4;
     // ONEB (ABL 2048, one bf16 term only): B of all 9 taps of a chunk in one buffer, one barrier per chunk (36 MFMAs per
     // wave between barriers instead of 12; the one-term chunk is too short to pay three barrier drains)
     constexpr bool ONEB = (ABL & 2048) != 0;
@@ -958,7 +1087,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
     constexpr bool HPAD = (2 * NS * HPXA * XBK + 2 * 3 * BGR * NS * XPLANE) * 2 + 7 * 256 * 4 <= 160 * 1024;
     constexpr int HPLANE = (HPAD ? HPXA : HPX) * XBK;   // bf16 per halo term plane
     constexpr int BPL = 3 * NS;                       // B planes per group (3 taps x NS terms)
-    constexpr int BQ = (BGR * BPL * 256 + HTHREADS - 1) / HTHREADS;  // 16-byte B pieces per thread
+    constexpr int BQ = (BGR * BPL * 256 + NTH - 1) / NTH;  // 16-byte B pieces per thread
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * NS * HPLANE + 2 * BGR * BPL * XPLANE];
     __bf16* Hs = smem;                                // [buf][term][halo pixel][16 ch] (xoff swizzle)
     __bf16* Bs = smem + 2 * NS * HPLANE;              // [buf][tap dx][term][col][16 k] (xoff swizzle)
@@ -990,14 +1119,14 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
     constexpr int NCOEF = PRE::kind == 1 ? 7 : (PRE::kind == 2 ? 2 : 0);
     __shared__ __attribute__((aligned(16))) float bcs[NCOEF ? NCOEF * 256 : 4];
     if constexpr (NCOEF > 0) {
-        for (int i = tid; i < NCOEF * Cin; i += HTHREADS) {
+        for (int i = tid; i < NCOEF * Cin; i += NTH) {
             const int k = i / Cin;
             bcs[i] = pre.p[k][i - k * Cin];
         }
         __syncthreads();
     }
 
-    f32x16 acc[2][2];
+    f32x16 acc[MI][2];
 
     // ---- halo staging: piece q = (halo pixel q>>2, channels 4(q&3)..+3); addresses fixed per block ----
     // Every global load of the main loop is issued unconditionally (pieces outside the image load a valid dummy
@@ -1016,10 +1145,10 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
     RawX yreg[PRE::on ? HQ : 1];    // PreBnBwd: the pre-norm activations of piece j
     unsigned hyo[PRE::on ? HQ : 1];
     auto setup_tile = [&](int t) {  // halo source offsets of tile t
-        const int m0 = t * HBM_, img = m0 / hw, h0 = (m0 - img * hw) / WT;
+        const int m0 = t * HB, img = m0 / hw, h0 = (m0 - img * hw) / WT;
 #pragma unroll
         for (int j = 0; j < HQ; ++j) {
-            const int q = tid + j * HTHREADS;
+            const int q = tid + j * NTH;
             const int hp = q >> 2, c4 = q & 3;
             const int hr = hp / HC, hc = hp - hr * HC;
             const int ih = h0 - 1 + hr, iw = hc - 1;
@@ -1032,7 +1161,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
     };
 #pragma unroll
     for (int j = 0; j < HQ; ++j) {
-        const int q = tid + j * HTHREADS;
+        const int q = tid + j * NTH;
         hdst[j] = (HPAD || q < HPX * 4) ? xoff(q >> 2, (q & 3) * 4) : -1;
     }
     setup_tile(t_first);
@@ -1084,7 +1213,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
                     if (pre.dyo != nullptr && blockIdx.y == 0) {   // block-uniform
                         // piece j's halo pixel (hr, hc) is one of the tile's own output pixels: rows 1..ROWS, columns
                         // 1..WT of the halo (always inside the image); hxo[j] addresses it in g, same layout as dyo
-                        const int q = tid + j * HTHREADS, hp = q >> 2, hr = hp / HC, hc = hp - hr * HC;
+                        const int q = tid + j * NTH, hp = q >> 2, hr = hp / HC, hc = hp - hr * HC;
                         if (q < HPX * 4 && hr >= 1 && hr <= ROWS && hc >= 1 && hc <= WT) {
                             char* o = reinterpret_cast<char*>(pre.dyo) + hxo[j] + (size_t)cc * 16 * XSZ;
                             if constexpr (std::is_same<XT, float>::value)
@@ -1135,7 +1264,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
     unsigned bpo[BQ];
 #pragma unroll
     for (int j = 0; j < BQ; ++j) {
-        const int q = tid + j * HTHREADS;
+        const int q = tid + j * NTH;
         // ONEB: plane pl = kernel row * BPL + tap (NS == 1); group gr of the chunk at the global group stride
         const int plg = min(q >> 8, BGR * BPL - 1), gr = plg / BPL, pl = plg - gr * BPL;
         const int dx = pl / NS, t = pl - dx * NS, half = q & 1;
@@ -1159,7 +1288,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
         __bf16* base = Bs + boff;
 #pragma unroll
         for (int j = 0; j < BQ; ++j) {
-            const int q = tid + j * HTHREADS;
+            const int q = tid + j * NTH;
             if (q < BGR * BPL * 256)
                 *reinterpret_cast<u32x4*>(base + (q >> 8) * XPLANE + xoff((q & 255) >> 1, (q & 1) * 8)) = breg[j];
         }
@@ -1167,23 +1296,31 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
 
     // per-lane halo pixel of each A fragment row (tap (0,0) origin)
     const int kh = (lane >> 5) * 8;
-    int hp0[2];
+    int hp0[MI];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int p = wm * 64 + 32 * i + (lane & 31);
+    for (int i = 0; i < MI; ++i) {
+        const int p = wm * (32 * MI) + 32 * i + (lane & 31);
         const int r = p / WT, c = p - r * WT;
         hp0[i] = r * HC + c;
     }
     int boff[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) boff[j] = xoff(wn * 64 + 32 * j + (lane & 31), kh);
-    int aoff[3][3][2];              // A fragment offset of tap (dy, dx), row block i (fixed per lane)
+    // A fragment offset of tap (dy, dx), row block i (fixed per lane); TALL computes them per kernel row instead
+    // (36 registers held across the loop would not fit beside the 128 accumulators)
+    int aoff[3][3][TALL ? 1 : 2];
+    if constexpr (!TALL) {
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
+        for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-        for (int dx = 0; dx < 3; ++dx)
+            for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
-            for (int i = 0; i < 2; ++i) aoff[dy][dx][i] = xoff(hp0[i] + dy * HC + dx, kh);
+                for (int i = 0; i < 2; ++i) aoff[dy][dx][i] = xoff(hp0[i] + dy * HC + dx, kh);
+    }
+    auto afrag = [&](int dy, int dx, int i) {
+        if constexpr (TALL) return xoff(hp0[i] + dy * HC + dx, kh);
+        else return aoff[dy][dx][i];
+    };
 
     auto hmfma = [&](const bf16x8& fa_, const bf16x8& fb_, const f32x16& c_) {
         if constexpr (ABL & 2) return xmfma<NT>(fa_, fb_, xmfma<NT>(fa_, fb_, c_));
@@ -1204,14 +1341,14 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
             }
         };
         // register double buffer: the fragments of tap dx+1 are read while the MFMAs of tap dx issue
-        bf16x8 FA[2][2][NS], FB[2][2][NS];
+        bf16x8 FA[2][MI][NS], FB[2][2][NS];
         auto ldfrag = [&](int buf, int dx) {
 #pragma unroll
             for (int t = 0; t < NS; ++t)
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    FA[buf][i][t] = *reinterpret_cast<const bf16x8*>(a + t * HPLANE + aoff[dy][dx][i]);
-                    FB[buf][i][t] = *reinterpret_cast<const bf16x8*>(b + (dx * NS + t) * XPLANE + boff[i]);
+                for (int i = 0; i < MI; ++i) {
+                    FA[buf][i][t] = *reinterpret_cast<const bf16x8*>(a + t * HPLANE + afrag(dy, dx, i));
+                    if (i < 2) FB[buf][i][t] = *reinterpret_cast<const bf16x8*>(b + (dx * NS + t) * XPLANE + boff[i]);
                 }
         };
         constexpr bool PREFETCH = ABL & 1;
@@ -1227,7 +1364,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
             const auto& fb = FB[dx & 1];
             // term-major: the hh products issue first, the cross terms after
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < MI; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[i][j] = hmfma(fa[i][0], fb[j][0], acc[i][j]);
             if constexpr (NT >= 3) {
@@ -1252,7 +1389,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
         }
         if constexpr (PREFETCH) {
             // pin the interleave: the next tap's fragment reads go one per MFMA gap of the current tap
-            constexpr int MF = 4 * (NT >= 6 ? 6 : (NT >= 3 ? 3 : 1)), RD = 4 * NS;
+            constexpr int MF = 2 * MI * (NT >= 6 ? 6 : (NT >= 3 ? 3 : 1)), RD = (MI + 2) * NS;
             if constexpr (V > 0) __builtin_amdgcn_sched_group_barrier(0x020, BQ, 0);   // next B loads first
             __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);          // tap 0 fragments
 #pragma unroll
@@ -1310,7 +1447,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
     for (int kt = 0, t = t_first; kt < tpb && t < mtiles; ++kt, t += t_step) {
     const bool nextt = kt + 1 < tpb && t + t_step < mtiles;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -1355,7 +1492,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
         compute(1, a, bcur + BPL * XPLANE, V0{});
         // staggered (stg): waves 4-7 split + store the next chunk before the last kernel row's MFMAs, waves 0-3 after
         // them (both buffers idle since the previous chunk's barrier)
-        const bool early = stg && __builtin_amdgcn_readfirstlane(wave) >= 4;   // wave-uniform (scalar branch)
+        const bool early = stg && __builtin_amdgcn_readfirstlane(wave) >= NTH / 128;   // wave-uniform (scalar branch)
         if (morec && early) { store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1); store_b((bb ^ 1) * 3 * BPL * XPLANE, bregA); }
         compute(2, a, bcur + 2 * BPL * XPLANE, V0{});
         if (morec && !early) { store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1); store_b((bb ^ 1) * 3 * BPL * XPLANE, bregA); }
@@ -1388,7 +1525,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
         // staggered split (ABL 256, or stg at run time: $CDM_HALO_STAGGER): waves 0-3 split + store the next halo
         // after this kernel row's MFMAs, waves 4-7 before them, so each SIMD pairs one wave's VALU with its partner's
         // MFMAs (wave-uniform)
-        const bool late = ((ABL & 256) || stg) && wave < 4;
+        const bool late = ((ABL & 256) || stg) && wave < NTH / 128;
         if constexpr (!(ABL & 1024)) {
             if (morec && !late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
         }
@@ -1406,7 +1543,7 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
         hb ^= 1;
     }
     }
-    unscale<NT>(acc, sx, op_scale<NT>(amax_w));
+    if constexpr (!TALL) unscale<NT>(acc, sx, op_scale<NT>(amax_w));   // (one term: unscaled)
     if (!DEEP && nextt) {   // the next tile's chunk 0 (its loads were issued during the last chunk) into the halo / B buffers
         // idle since the last chunk's closing barrier, ahead of the epilogue: its prefetch registers die before the
         // epilogue and the epilogue needs no barrier pair after it
@@ -1415,7 +1552,11 @@ __global__ __launch_bounds__(HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* 
     }
     // epilogue scratch (stats / max-min: 4 KiB): the other halo buffer (>= 24 KiB), last read by the final chunk
     // before its closing barrier
-    ep(acc, t * HBM_ + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(Hs + (hb ^ 1) * NS * HPLANE), tid);
+    if constexpr (TALL)
+        ep.tall(acc, t * HB + wm * 128, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(Hs + (hb ^ 1) * NS * HPLANE),
+                tid);
+    else
+        ep(acc, t * HB + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(Hs + (hb ^ 1) * NS * HPLANE), tid);
     if (nextt) __syncthreads();
     }
 }
