@@ -389,16 +389,18 @@ __global__ __launch_bounds__(256) void conv_cin1_dgrad_kernel(const float* g1, i
 // HPM: halo pixels the LDS images hold, (R + 2) W rounded up to 64: 384 for W <= 64 (40 KiB of LDS, 4 blocks per CU;
 // the W-independent 768-pixel images took 80 KiB, 2 blocks per CU, half the loads in flight: 2.3 TB/s), 512 for W = 128,
 // 768 for W = 256
-// HPM threads per block, one halo pixel each in the tap reduction (256 threads over 384 halo pixels left half the
-// waves with a second pixel: the SIMDs holding waves 0-1 did twice the FMAs of the others)
-template <int HPM>
-__global__ __launch_bounds__(HPM) void conv_cout1_fwd_band_kernel(const float* __restrict__ z, int ldz, int H, int W,
+// FULL = false (default): 256 threads, up to HPM / 256 halo pixels per thread in the tap reduction (at 384 pixels the
+// SIMDs holding waves 0-1 do twice the FMAs of the others).  FULL ($CDM_COUT1_FULL=1): HPM threads, one halo pixel
+// each — balanced SIMDs, but same-box 182 vs 164 us per C2 step (profiles/r4_ab_cout1_threads.txt)
+template <int HPM, bool FULL = true>
+__global__ __launch_bounds__(FULL ? HPM : 256) void conv_cout1_fwd_band_kernel(const float* __restrict__ z, int ldz, int H, int W,
                                                                   int C, const float* __restrict__ w,
                                                                   const float* __restrict__ bias,
                                                                   float* __restrict__ out,
                                                                   const float* __restrict__ gs,
                                                                   const float* __restrict__ gt) {
-    constexpr int KQ = 1;                             // halo pixels per thread in the tap reduction
+    constexpr int NTHR = FULL ? HPM : 256;
+    constexpr int KQ = (HPM + NTHR - 1) / NTHR;       // halo pixels per thread in the tap reduction
     __shared__ float zt[HPM * 17];                    // [halo px][16 ch + 1 pad]
     __shared__ float st[9 * HPM];                     // [tap][halo px]
     const int R = 256 / W, HP = (R + 2) * W;
@@ -414,11 +416,11 @@ __global__ __launch_bounds__(HPM) void conv_cout1_fwd_band_kernel(const float* _
         for (int t = 0; t < 9; ++t) acc[k][t] = 0.f;
     // staging: piece i of this thread = (halo pixel q4>>2, channels 4(q4&3)..+3) of the current 16-channel slab;
     // the next slab's pieces are loaded into registers while this slab is reduced (one slab of latency hidden)
-    constexpr int PQ = 4;                             // HPM * 4 pieces over HPM threads
+    constexpr int PQ = HPM * 4 / NTHR;               // HPM * 4 pieces over the threads
     const float* src[PQ];
 #pragma unroll
     for (int i = 0; i < PQ; ++i) {
-        const int q4 = tid + i * HPM, q = q4 >> 2, part = q4 & 3;
+        const int q4 = tid + i * NTHR, q = q4 >> 2, part = q4 & 3;
         const int hh = h0 - 1 + q / W, ww = q - (q / W) * W;
         src[i] = (q < HP && (unsigned)hh < (unsigned)H) ? z + (((long long)n * H + hh) * W + ww) * ldz + part * 4
                                                         : nullptr;
@@ -438,7 +440,7 @@ __global__ __launch_bounds__(HPM) void conv_cout1_fwd_band_kernel(const float* _
         }
 #pragma unroll
         for (int i = 0; i < PQ; ++i) {
-            const int q4 = tid + i * HPM;
+            const int q4 = tid + i * NTHR;
             if ((q4 >> 2) < HP) {
                 float v[4] = {pre[i].x, pre[i].y, pre[i].z, pre[i].w};
                 if (gs && src[i]) {
@@ -453,7 +455,7 @@ __global__ __launch_bounds__(HPM) void conv_cout1_fwd_band_kernel(const float* _
         if (c0 + 16 < C) gload(c0 + 16);
 #pragma unroll
         for (int k = 0; k < KQ; ++k) {
-            const int q = tid + k * HPM;
+            const int q = tid + k * NTHR;
             if (q < HP) {
 #pragma unroll
                 for (int c = 0; c < 16; ++c) {
@@ -467,7 +469,7 @@ __global__ __launch_bounds__(HPM) void conv_cout1_fwd_band_kernel(const float* _
     }
 #pragma unroll
     for (int k = 0; k < KQ; ++k) {
-        const int q = tid + k * HPM;
+        const int q = tid + k * NTHR;
         if (q < HP) {
 #pragma unroll
             for (int t = 0; t < 9; ++t) st[t * HP + q] = acc[k][t];
@@ -475,7 +477,7 @@ __global__ __launch_bounds__(HPM) void conv_cout1_fwd_band_kernel(const float* _
     }
     __syncthreads();
     // output pixel (h0 + r, c): sum over taps of the partial of halo pixel (r + ky, c + kx - 1)
-    if (tid >= 256) return;
+    if (FULL && tid >= 256) return;
     const int r = tid / W, c = tid - r * W;
     float o = bias[0];
 #pragma unroll
@@ -752,10 +754,11 @@ __global__ __launch_bounds__(256) void embed_bwd_act_kernel(Mlp4 P) {
 
 // parameter grads (assign): dw2[j][i], db2[j], dw1[i][k], db1[i]; each a sequential fp64 sum over the rows (the
 // product of two fp32 values is exact in fp64, so fma and multiply-add give the same bits).  dw2 (E x E outputs, the
-// bulk) in 32 x 32 tiles (160 blocks for the four MLPs at n_feat 128): the block stages 64 rows of dout and h through
-// LDS and each thread carries 2 x 2 outputs (the per-output form waited on one global load per row: 40 us per C2 step,
-// latency-bound; 64 x 64 tiles ran 40 blocks, 30 us); blocks past the tiles take db2, dw1, db1 one output per thread.
-constexpr int EMB_T = 32, EMB_R = 64;
+// bulk) in 64 x 64 tiles: the block stages 64 rows of dout and h through LDS and each thread carries 4 x 4 outputs, 16
+// independent fp64 chains (the per-output form waited on one global load per row: 40 us per C2 step, latency-bound);
+// blocks past the tiles take db2, dw1, db1 one output per thread.  30 us per C2 step; 32 x 32 tiles (160 blocks, 4
+// chains per thread) measured 67 us (fp64 FMA latency with a quarter of the chains, profiles/r4_train_step_*).
+constexpr int EMB_T = 64;
 static __host__ __device__ inline int embed_tiles(int E) { return ((E + EMB_T - 1) / EMB_T) * ((E + EMB_T - 1) / EMB_T); }
 __global__ __launch_bounds__(256) void embed_bwd_param_kernel(Mlp4 P) {
     const MlpDesc& d = P.m[blockIdx.y];
@@ -763,45 +766,48 @@ __global__ __launch_bounds__(256) void embed_bwd_param_kernel(Mlp4 P) {
     const int nt = embed_tiles(E);
     const int tid = threadIdx.x;
     if ((int)blockIdx.x < nt) {
-        __shared__ __attribute__((aligned(16))) float ds_[EMB_R][EMB_T], hs_[EMB_R][EMB_T];
+        __shared__ __attribute__((aligned(16))) float ds_[EMB_T][EMB_T], hs_[EMB_T][EMB_T];
         const int tpr = (E + EMB_T - 1) / EMB_T;
         const int j0 = (blockIdx.x / tpr) * EMB_T, i0 = (blockIdx.x % tpr) * EMB_T;
-        const int tj = (tid >> 4) * 2, ti = (tid & 15) * 2;
-        double s[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
-        constexpr int PER = EMB_R * EMB_T / 256;
-        for (int b0 = 0; b0 < rows; b0 += EMB_R) {
-            const int nb = min(EMB_R, rows - b0);
-            // the chunk's 2 x PER loads per thread issued together (then stored): one memory latency per chunk
-            float dv_[PER], hv_[PER];
+        const int tj = (tid >> 4) * 4, ti = (tid & 15) * 4;
+        double s[4][4];
 #pragma unroll
-            for (int u = 0; u < PER; ++u) {
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) s[a][c] = 0.0;
+        for (int b0 = 0; b0 < rows; b0 += EMB_T) {
+            const int nb = min(EMB_T, rows - b0);
+            // the chunk's 2 x 16 loads per thread issued together (then stored): one memory latency per chunk
+            float dv_[EMB_T * EMB_T / 256], hv_[EMB_T * EMB_T / 256];
+#pragma unroll
+            for (int u = 0; u < EMB_T * EMB_T / 256; ++u) {
                 const int q = tid + u * 256, r = q / EMB_T, c = q - r * EMB_T;
                 const bool ok = r < nb;
                 dv_[u] = ok && j0 + c < E ? d.dout[(long long)(b0 + r) * E + j0 + c] : 0.f;
                 hv_[u] = ok && i0 + c < E ? d.h[(long long)(b0 + r) * E + i0 + c] : 0.f;
             }
 #pragma unroll
-            for (int u = 0; u < PER; ++u) {
+            for (int u = 0; u < EMB_T * EMB_T / 256; ++u) {
                 const int q = tid + u * 256, r = q / EMB_T, c = q - r * EMB_T;
                 ds_[r][c] = dv_[u];
                 hs_[r][c] = hv_[u];
             }
             __syncthreads();
             for (int r = 0; r < nb; ++r) {
-                const float2 dv = *reinterpret_cast<const float2*>(&ds_[r][tj]);
-                const float2 hv = *reinterpret_cast<const float2*>(&hs_[r][ti]);
-                const double dd[2] = {dv.x, dv.y}, hh[2] = {hv.x, hv.y};
+                const float4 dv = *reinterpret_cast<const float4*>(&ds_[r][tj]);
+                const float4 hv = *reinterpret_cast<const float4*>(&hs_[r][ti]);
+                const double dd[4] = {dv.x, dv.y, dv.z, dv.w}, hh[4] = {hv.x, hv.y, hv.z, hv.w};
 #pragma unroll
-                for (int a = 0; a < 2; ++a)
+                for (int a = 0; a < 4; ++a)
 #pragma unroll
-                    for (int c = 0; c < 2; ++c) s[a][c] = fma(dd[a], hh[c], s[a][c]);
+                    for (int c = 0; c < 4; ++c) s[a][c] = fma(dd[a], hh[c], s[a][c]);
             }
             __syncthreads();
         }
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
+            for (int c = 0; c < 4; ++c) {
                 const int j = j0 + tj + a, i = i0 + ti + c;
                 if (j < E && i < E) d.dw2[(long long)j * E + i] = (float)s[a][c];
             }
@@ -1142,6 +1148,16 @@ static int launch_cout1_band(const float* z, int ldz, int N, int H, int W, int C
                              float* out, const float* gs, const float* gt, hipStream_t st) {
     const dim3 grid(N * (H / (256 / W)));
     const int hp = (256 / W + 2) * W;           // halo pixels of a band
+    static const int full = [] { const char* e = getenv("CDM_COUT1_FULL"); return e ? atoi(e) : 0; }();
+    if (!full) {
+        if (hp <= 384)
+            hipLaunchKernelGGL((conv_cout1_fwd_band_kernel<384, false>), grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
+        else if (hp <= 512)
+            hipLaunchKernelGGL((conv_cout1_fwd_band_kernel<512, false>), grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
+        else
+            hipLaunchKernelGGL((conv_cout1_fwd_band_kernel<768, false>), grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
+        return cdm_status();
+    }
     if (hp <= 384)
         hipLaunchKernelGGL(conv_cout1_fwd_band_kernel<384>, grid, dim3(384), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
     else if (hp <= 512)
