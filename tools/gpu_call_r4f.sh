@@ -1,9 +1,8 @@
-# round 4 (f): T=1500 excess — substitute eps / yO; baseline with fp64 embeddings
+# round 4 (f): final at HEAD after the tail-kernel reverts — full GPU suite at the round's defaults, the bench (driver command), smoke()
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
-for ov in none eps yO; do
-  echo "=== override $ov"
-  if [ $ov = none ]; then args=""; else args="--override $ov"; fi
-  timeout -k 10 300 python -u tools/t1500_steps.py --w 0 --window 1500 $args > gpurun_out/r4f_ov_$ov.txt 2>&1 || { tail -20 gpurun_out/r4f_ov_$ov.txt; exit 1; }
-  tail -2 gpurun_out/r4f_ov_$ov.txt
-done
+CDM_PARITY_OUT=gpurun_out/r4f_parity.jsonl timeout -k 10 900 python -u -m pytest -v --timeout 600 --timeout-method thread -m gpu tests/ > gpurun_out/r4f_gpu_tests.log 2>&1; echo "gpu tests rc=$?"
+grep -E "FAILED|Error|passed|failed" gpurun_out/r4f_gpu_tests.log | tail -8
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r4f_smoke.txt 2>&1; echo "smoke rc=$?"; tail -2 gpurun_out/r4f_smoke.txt
+timeout -k 10 900 python -u bench.py > gpurun_out/r4f_bench.json 2> gpurun_out/r4f_bench.err || { echo "bench failed"; tail -20 gpurun_out/r4f_bench.err; exit 1; }
+head -c 700 gpurun_out/r4f_bench.json; echo
 echo ALL_DONE
