@@ -471,6 +471,60 @@ def stats_rate(n: int):
             "cpu_reference_ms_per_map": round(cpu_ms, 3), "cpu_sample": "8 maps, numpy (1 thread, the reference loop)"}
 
 
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` with no rank environment (WORLD_SIZE unset): run the N ranks as ONE child process tree,
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py <same args>`, inheriting stdout (rank 0 prints the
+    JSON line) and stderr, and return its exit status.  Called before anything touches the GPU, and never replaces this
+    process (no exec): the parent only waits."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:                      # a free rendezvous port on the loopback interface
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    _progress(f"--gpus {n}: launching {n} ranks (torch.distributed.run, rendezvous 127.0.0.1:{port})")
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def plumbing_check(args, world: int, rank: int):
+    """CPU rehearsal of the N-rank harness (--plumbing-check; tests/test_bench_cpu.py): gloo process group, the world
+    size check, barrier-bracketed timing of K steps with the max over ranks, rank-0 JSON — with a stand-in CPU step (a
+    small matmul) instead of the GPU workload.  Not a measurement: the line says so in `metric` and `plumbing_only`."""
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    a = torch.randn(64, 64)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+    for _ in range(args.warmup):
+        a = torch.tanh(a @ a)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        a = torch.tanh(a @ a)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank == 0:
+        print(json.dumps({"metric": "plumbing check (no measurement)", "plumbing_only": True, "value": None,
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(dt / max(args.steps, 1) * 1e3, 4),
+                          "config": {"parallelism": f"dp{world}", "batch_per_gpu": args.batch,
+                                     "global_batch": args.batch * world}}), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -491,9 +545,22 @@ def main():
                          "mask and the cgroup CPU quota)")
     ap.add_argument("--conv-math", choices=sorted(CONV_MATH_INFO), default="h3",
                     help="3x3 conv arithmetic of the C2 / C5 legs (fp32-accurate; see DESIGN.md §3)")
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="CPU-only rehearsal of the N-rank launch / timing / JSON path (gloo, stand-in step; no GPU)")
     args = ap.parse_args()
 
+    # --gpus N: the ranks come from the environment of torch.distributed.run; without one, this process launches them
+    # (before any GPU call) and relays their exit status
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = _dist_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if args.plumbing_check:
+        plumbing_check(args, world, rank)
+        return
     # rehearsal of the N>1 path on a one-GPU box: CDM_BENCH_REHEARSE=1 puts every rank on cuda:0 and runs the
     # collectives over gloo (RCCL refuses two ranks on one device); never set by the driver's runs
     rehearse = os.environ.get("CDM_BENCH_REHEARSE") == "1"
@@ -507,6 +574,8 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     import cdm_amd  # noqa: F401
 
     def barrier():

@@ -9,6 +9,8 @@
 // the order the caller's index list gives (CSR), so the reference's flat-order sums are reproduced exactly.
 #include "cdm_common.h"
 
+#include <type_traits>
+
 namespace cdm {
 
 // pass 1: T[b][x][v] = sum_y img[b][x][y] * w^(v*y),  w = exp(-2 pi i / N); one block per (b, x), thread v
@@ -67,8 +69,9 @@ __global__ void dft_cols_power_kernel(const double2* __restrict__ T, int N, doub
 // Any-rank boxes (power_spectrum's 3-D branch and non-square 2-D boxes, diffusion_utilities.py:316-336): the DFT
 // along one axis of a complex fp64 array viewed as [outer][n][inner], one thread per output element (o, k, i):
 // out[o][k][i] = sum_j in[o][j][i] w^(k j).  Successive calls over every axis give fftn.  The input of the first pass is
-// the real fp32 box (re only); the last pass may write |F|^2 * scale instead of F.
-template <bool REAL_IN, bool POWER_OUT>
+// the real box (re only: fp32, or fp64 as numpy's fftn of a float64 array computes); the last pass may write
+// |F|^2 * scale instead of F.  RealT = void: complex fp64 input (the later passes).
+template <typename RealT, bool POWER_OUT>
 __global__ __launch_bounds__(256) void dft_axis_kernel(const void* __restrict__ in_, int outer, int n, long long inner,
                                                        double scale, void* __restrict__ out_) {
     extern __shared__ double tw[];            // [2n]: cos, sin of 2 pi k / n
@@ -90,8 +93,8 @@ __global__ __launch_bounds__(256) void dft_axis_kernel(const void* __restrict__ 
     int idx = 0;
     for (int j = 0; j < n; ++j) {             // w^(k j): angle index (k*j) mod n, accumulated
         const double c = tw[idx], sn = tw[n + idx];
-        if constexpr (REAL_IN) {
-            const double v = (double)static_cast<const float*>(in_)[base + (long long)j * inner];
+        if constexpr (!std::is_void_v<RealT>) {
+            const double v = (double)static_cast<const RealT*>(in_)[base + (long long)j * inner];
             re = fma(v, c, re);
             im = fma(-v, sn, im);
         } else {                              // (a + i b)(c - i s)
@@ -179,8 +182,9 @@ CDM_API int cdm_dft2_power(const float* img, int B, int N, double scale, void* T
 
 // |fftn(box[b])|^2 * scale for B row-major boxes of rank 1..3 with extents dims[0..rank); T0 / T1 = scratch of
 // B * prod(dims) complex doubles each (ping-pong between the axis passes)
-CDM_API int cdm_dftn_power(const float* box, int B, int rank, const int* dims, double scale, void* T0, void* T1,
-                           double* power, void* stream) {
+template <typename RealT>
+static int dftn_power(const RealT* box, int B, int rank, const int* dims, double scale, void* T0, void* T1,
+                      double* power, void* stream) {
     if (B < 0 || rank < 1 || rank > 3) return (int)hipErrorInvalidValue;
     long long n_all = 1;
     for (int a = 0; a < rank; ++a) {
@@ -201,21 +205,32 @@ CDM_API int cdm_dftn_power(const float* box, int B, int rank, const int* dims, d
         const bool first = a == 0, last = a == rank - 1;
         void* dst = last ? (void*)power : bufs[a & 1];
         if (first && last)
-            hipLaunchKernelGGL((dft_axis_kernel<true, true>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
+            hipLaunchKernelGGL((dft_axis_kernel<RealT, true>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
                                scale, dst);
         else if (first)
-            hipLaunchKernelGGL((dft_axis_kernel<true, false>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
+            hipLaunchKernelGGL((dft_axis_kernel<RealT, false>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
                                scale, dst);
         else if (last)
-            hipLaunchKernelGGL((dft_axis_kernel<false, true>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
+            hipLaunchKernelGGL((dft_axis_kernel<void, true>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
                                scale, dst);
         else
-            hipLaunchKernelGGL((dft_axis_kernel<false, false>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
+            hipLaunchKernelGGL((dft_axis_kernel<void, false>), grid, dim3(256), sm, SS(stream), src, outer, n, inner,
                                scale, dst);
         int e = cdm_status(); if (e) return e;
         src = dst;
     }
     return 0;
+}
+
+CDM_API int cdm_dftn_power(const float* box, int B, int rank, const int* dims, double scale, void* T0, void* T1,
+                           double* power, void* stream) {
+    return dftn_power(box, B, rank, dims, scale, T0, T1, power, stream);
+}
+
+// the same for fp64 boxes (np.fft.fftn of a float64 array: no fp32 rounding of the input)
+CDM_API int cdm_dftn_power_f64(const double* box, int B, int rank, const int* dims, double scale, void* T0, void* T1,
+                               double* power, void* stream) {
+    return dftn_power(box, B, rank, dims, scale, T0, T1, power, stream);
 }
 
 CDM_API int cdm_bin_sum(const double* power, int B, long long NN, const int* off, const int* idx, int nbins,

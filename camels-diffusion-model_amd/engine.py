@@ -374,6 +374,12 @@ class UNetEngine:
         return ((l.cin == 1 or halo(l)) and halo(c) and c.cin == l.cout and c.cin <= 256 and c.cin % 128 == 0
                 and c.cout % 128 == 0 and c.S == l.S)
 
+    def fuses_gn_out(self, train: bool) -> bool:
+        """out.1's GroupNorm + ReLU runs inside out.3's kernels (forward; train: and its weight gradient): zO is never
+        written, and its workspace buffer is not allocated."""
+        nf, H = self.nf, self.H
+        return (not train or self.fuse_gn_out) and nf % 16 == 0 and H <= 256 and 256 % H == 0
+
     def fuses_bn_bwd(self, l: "LayerSpec", kind: str, B: int = 1) -> bool:
         """Layer l's BN backward runs inside its dgrad / wgrad staging (cdm_conv3x3_*_h3_bnbwd)."""
         return (self.fuse_bn_bwd and kind in ("dense", "plain", "resid") and l.cin > 1
@@ -409,8 +415,11 @@ class UNetEngine:
         return self._dst_slot(ws, prev)
 
     # ------------------------------------------------------------------------------------------
-    def workspace(self, B: int, train: bool) -> "Workspace":
-        return Workspace(self, B, train)
+    def workspace(self, B: int, train: bool, frozen: bool = False) -> "Workspace":
+        """frozen: a train-structured workspace for the forward / backward of model.eval() under autograd (BatchNorm on
+        the running statistics); it keeps fp32 activations under C4's bf16 arithmetic, like the no-grad eval path, so an
+        eval model returns the same eps whether or not autograd records it."""
+        return Workspace(self, B, train, frozen)
 
     # ------------------------------------------------------------------------------------------
     # forward
@@ -429,6 +438,7 @@ class UNetEngine:
         H1, H2 = H // 2, H // 4
         train = ws.train
         assert train or not frozen
+        assert not (frozen and ws.act16), "eval-mode forwards keep fp32 activations: use workspace(B, True, frozen=True)"
         ws.frozen = frozen
         eps = out if out is not None else ws.eps
         ws.x_in = x
@@ -499,7 +509,7 @@ class UNetEngine:
                      _p(ws.slab), nf, self.kc_out0, s, amax_x=self._slot(ws, "catO"))
         probe("yO", ws)
         self._gn_fwd(ws, P, "out.1", Act(ws.yO, nf), B, H, nf, ws.gnO, stats_from_conv=True, stream=s)
-        if (not train or self.fuse_gn_out) and nf % 16 == 0 and H <= 256 and 256 % H == 0:
+        if self.fuses_gn_out(train):
             # out.1's GroupNorm + ReLU applied in out.3's staging (train: and in out.3's weight gradient): zO never
             # written
             lb.cdm_conv3x3_cout1_fwd_gn(_p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]), _p(ws.gnO["shift"]),
@@ -1056,7 +1066,7 @@ def ctypes_addr(obj):
 class Workspace:
     """All device buffers for one batch size and mode (train keeps what backward needs)."""
 
-    def __init__(self, eng: UNetEngine, B: int, train: bool):
+    def __init__(self, eng: UNetEngine, B: int, train: bool, frozen: bool = False):
         self.eng, self.B, self.train = eng, B, train
         self.frozen = False          # set by each forward (eval-mode BatchNorm in a train-structured forward)
         self.zO_fused = False        # set by each forward: out.1's GroupNorm + ReLU applied inside out.3's kernels
@@ -1073,7 +1083,8 @@ class Workspace:
         self.yT2 = E(P0, nf)
         self.y0 = E(P2, 2 * nf)
         self.yO = E(P0, nf)
-        self.zO = E(P0, nf)
+        # zO = relu(GN(yO)) only exists where out.3 cannot apply out.1 in its staging (537 MB at the bench shape)
+        self.zO = E(P0, nf) if not eng.fuses_gn_out(train) else torch.empty(0, device=dev)
         self.hsum, self.hpre, self.hv = E(B, 2 * nf), E(B, 2 * nf), E(B, 2 * nf)
         self.c_zero = torch.zeros(B, ncf, device=dev)
         self.emb = {m: E(B, (2 if m.endswith("1") else 1) * nf) for m in MLPS}
@@ -1203,7 +1214,7 @@ class Workspace:
             # staging, C_in > 1; each has its BN-backward sums fused into the consumer's weight gradient and a private
             # gradient buffer, so every kernel reading them is one of the two templated conv kernels)
             self.act16 = set()
-            if eng.act16:
+            if eng.act16 and not frozen:
                 self.act16 = {l.name for l in L if l.name in self.fused_fwd and l.cin > 1 and l.name in self.sums_by
                               and l.name in self.fused and self.gout[l.name].off == 0}
         else:

@@ -141,7 +141,7 @@ class _UNetFunction(torch.autograd.Function):
         B = x.shape[0]
         eng.repack(P, True, s)
         ctx.pack_token = eng.train_pack_token = object()   # whose weights the engine's train pack holds
-        ws = eng.workspace(B, True)
+        ws = eng.workspace(B, True, frozen=frozen)
         eps = eng.forward(ws, P, x.reshape(B, mod.h, mod.h), t, c, sc_w, sc_b, B, s, frozen=frozen)
         ctx.frozen = frozen
         mod._invalidate_eval_pack()

@@ -86,7 +86,7 @@ def _as_maps(images) -> torch.Tensor:
         x = x[None]
     if x.dim() != 3 or x.shape[1] != x.shape[2]:
         raise ValueError("expected square 2-D maps [B, N, N] / [B, 1, N, N] / [N, N]")
-    return x.to("cuda", torch.float32).contiguous()
+    return x.to(x.device if x.is_cuda else "cuda", torch.float32).contiguous()
 
 
 def _power(x: torch.Tensor, scale: float) -> torch.Tensor:
@@ -109,7 +109,7 @@ def _bin_sums(P: torch.Tensor, idx: np.ndarray, off: np.ndarray) -> torch.Tensor
 
 
 def _power_nd(x: torch.Tensor, dims, scale: float) -> torch.Tensor:
-    """|fftn|^2 * scale of B boxes x [B, *dims] (any rank <= 3, any extents): one DFT pass per axis."""
+    """|fftn|^2 * scale of B boxes x [B, *dims] (any rank <= 3, any extents; fp32 or fp64): one DFT pass per axis."""
     import ctypes
     B = x.shape[0]
     n = int(np.prod(dims))
@@ -117,8 +117,8 @@ def _power_nd(x: torch.Tensor, dims, scale: float) -> torch.Tensor:
     T1 = torch.empty(B * n * 2, dtype=torch.float64, device=x.device) if len(dims) > 2 else T0
     P = torch.empty(B, n, dtype=torch.float64, device=x.device)
     d = (ctypes.c_int * len(dims))(*dims)          # read by the host entry point before it returns
-    lib().cdm_dftn_power(x.data_ptr(), B, len(dims), ctypes.addressof(d), float(scale), T0.data_ptr(), T1.data_ptr(),
-                         P.data_ptr(), _s())
+    fn = lib().cdm_dftn_power_f64 if x.dtype == torch.float64 else lib().cdm_dftn_power
+    fn(x.data_ptr(), B, len(dims), ctypes.addressof(d), float(scale), T0.data_ptr(), T1.data_ptr(), P.data_ptr(), _s())
     return P
 
 
@@ -139,14 +139,18 @@ def power_spectra(images, dl: float = 1.0) -> Tuple[np.ndarray, torch.Tensor]:
 
 def power_spectrum(box, dl: float = 1.0):
     """diffusion_utilities.py:302-368 for a 2-D or 3-D box (any extents) -> (k_bins, pk) numpy."""
-    b = np.asarray(box.detach().cpu() if torch.is_tensor(box) else box)
-    if b.ndim not in (2, 3):
+    x = box if torch.is_tensor(box) else torch.from_numpy(np.asarray(box))
+    if x.dim() not in (2, 3):
         raise ValueError("Input box must be 2D or 3D")
-    if b.ndim == 2 and b.shape[0] == b.shape[1]:
-        k, pk = power_spectra(b, dl)
+    # np.fft.fftn computes in the input's precision: fp64 boxes (numpy's default) keep fp64 values, anything else fp32;
+    # a CUDA tensor stays on its device
+    f64 = x.dtype == torch.float64
+    if x.dim() == 2 and x.shape[0] == x.shape[1] and not f64:
+        k, pk = power_spectra(x, dl)
         return k, pk[0].cpu().numpy()
-    dims = tuple(int(v) for v in b.shape)
-    x = torch.from_numpy(np.ascontiguousarray(b, np.float32)).to("cuda").reshape(1, -1)
+    dims = tuple(int(v) for v in x.shape)
+    dev = x.device if x.is_cuda else torch.device("cuda")
+    x = x.detach().to(dev, torch.float64 if f64 else torch.float32).contiguous().reshape(1, -1)
     P = _power_nd(x, dims, 1.0 / float(np.prod(dims)))      # norm="ortho": |F|^2 / prod(dims)
     k, pk = _binned(P, dims, dl)
     return k, pk[0].cpu().numpy()

@@ -172,6 +172,10 @@ int cdm_dft2_power(const float* img, int B, int N, double scale, void* T, double
  * branches of power_spectrum (diffusion_utilities.py:316-336). */
 int cdm_dftn_power(const float* box, int B, int rank, const int* dims, double scale, void* T0, void* T1, double* power,
                    void* stream);
+/* cdm_dftn_power for fp64 boxes: power_spectrum of a float64 numpy box, whose np.fft.fftn runs on the fp64 values
+ * (diffusion_utilities.py:322) — no fp32 rounding of the input. */
+int cdm_dftn_power_f64(const double* box, int B, int rank, const int* dims, double scale, void* T0, void* T1,
+                       double* power, void* stream);
 /* out[b][k] = sum_{i = off[k]}^{off[k+1]-1} power[b][idx[i]] in list order (the reference's binning loops,
  * diffusion_utilities.py:352-356 / sample_power_spectra.py:157-163, with the bin geometry built on the host) */
 int cdm_bin_sum(const double* power, int B, long long NN, const int* off, const int* idx, int nbins, double* out,

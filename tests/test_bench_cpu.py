@@ -33,3 +33,34 @@ def test_pmc_traffic_missing_keys(tmp_path, monkeypatch):
     assert b.pmc_traffic("fp32") == 1234
     (prof / "r9_pmc_conv128_h3.json").write_text('{"FETCH_SIZE": 10, "WRITE_SIZE": 2}')
     assert b.pmc_traffic("h3") == int((10 / b.HALO_FETCH_PER_BYTE + 2) * 1024)
+
+
+def _run_bench(*args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=env)
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    return p.returncode, lines, p.stderr
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` (the driver's command shape, no rank environment) starts 2 ranks itself and relays rank 0's
+    single JSON line: n_gpus 2, parallelism dp2 (VERDICT r4 missing-1).  CPU rehearsal: --plumbing-check (gloo)."""
+    rc, lines, err = _run_bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--plumbing-check")
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1, lines
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 512
+    assert out["plumbing_only"] is True and out["value"] is None
+
+
+def test_bench_world_size_mismatch_fails():
+    """A rank environment that disagrees with --gpus exits non-zero instead of measuring the wrong world."""
+    rc, lines, _ = _run_bench("--gpus", "2", "--steps", "1", "--warmup", "0", "--plumbing-check",
+                              env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and not lines

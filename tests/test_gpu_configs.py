@@ -369,3 +369,53 @@ def test_c5_nf256_train_grads_vs_fp64():
     assert zero_ok
     assert max(errs.values()) <= 1e-2, worst
     assert float(np.median(list(errs.values()))) <= 5e-3
+
+
+def test_c4_bf16_eval_under_autograd_matches_no_grad_eval():
+    """model.eval() under autograd (the train-structured forward with BatchNorm frozen on the running
+    statistics) keeps fp32 activations under C4's bf16 arithmetic, like the no-grad eval path, so the same eval model
+    returns eps of the same accuracy whether or not autograd records it.  n_feat = 128 (the width whose fused chain
+    stores bf16 activations in train mode), B = 2: eps with and without grad, and the input / parameter gradients, vs
+    fp64 autograd of the oracle in eval mode, within 1.5x the oracle run under the same bf16 operand rounding."""
+    nf, B, H = 128, 2, 64
+    m = _model(nf, H, seed=5, math="bf16").eval()
+    sd = R.clone_sd(m.state_dict())
+    g = torch.Generator().manual_seed(19)
+    x = torch.randn(B, 1, H, H, generator=g); t = torch.rand(B, generator=g); c = torch.rand(B, 6, generator=g)
+    wgt = torch.randn(B, 1, H, H, generator=g)
+    with torch.no_grad():
+        torch.manual_seed(21)
+        eps_ng = m(x.cuda(), t.cuda(), c.cuda()).cpu()
+    xg = x.cuda().requires_grad_(True)
+    torch.manual_seed(21)
+    eps_g = m(xg, t.cuda(), c.cuda())
+    (eps_g * wgt.cuda()).sum().backward()
+    keys = [k for k, _, kind in R.state_dict_layout(1, nf, 6, H) if kind == "param"]
+
+    def oracle(dtype):
+        s = {k: (v.to(dtype) if v.is_floating_point() else v.clone()).clone() for k, v in sd.items()}
+        for k in keys:
+            s[k].requires_grad_(True)
+        xx = x.to(dtype).clone().requires_grad_(True)
+        torch.manual_seed(21)
+        w_, b_ = R.draw_shortcut(1, nf)
+        e = R.unet_forward(s, xx, t.to(dtype), c.to(dtype), n_feat=nf, n_cfeat=6, height=H, train=False,
+                           shortcut=(w_.to(dtype), b_.to(dtype)))
+        (e * wgt.to(dtype)).sum().backward()
+        return e.detach(), xx.grad, {k: s[k].grad for k in keys}
+    e64, dx64, g64 = oracle(torch.float64)
+    with _bf16_operands():
+        eem, dxem, gem = oracle(torch.float32)
+    e_ng, e_g, e_em = _rel(eps_ng, e64), _rel(eps_g, e64), _rel(eem, e64)
+    rl2 = lambda a, b: ((a.detach().double().cpu() - b.double()).norm() / b.double().norm()).item()   # noqa: E731
+    errs = {k: rl2(p.grad, g64[k]) for k, p in m.named_parameters() if g64[k].norm() > 0}
+    errs_em = {k: rl2(gem[k], g64[k]) for k in errs}
+    dx_err, dx_em = rl2(xg.grad.view(B, 1, H, H), dx64), rl2(dxem, dx64)
+    print(f"eval bf16 eps no-grad {e_ng:.2e} / grad {e_g:.2e} / emulated {e_em:.2e}; dx {dx_err:.2e} / {dx_em:.2e}; "
+          f"grads max {max(errs.values()):.2e} / {max(errs_em.values()):.2e}")
+    _parity.record("c4_eval_under_autograd", eps_no_grad=e_ng, eps_grad=e_g, eps_emulated=e_em, dx=dx_err,
+                   dx_emulated=dx_em, grad_max=max(errs.values()), grad_max_emulated=max(errs_em.values()))
+    assert e_ng <= 1.5 * e_em and e_g <= 1.5 * e_em
+    assert dx_err <= 1.5 * dx_em
+    assert max(errs.values()) <= 1.5 * max(errs_em.values())
+    assert float(np.median(list(errs.values()))) <= 1.5 * float(np.median(list(errs_em.values())))

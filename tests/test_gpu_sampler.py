@@ -170,11 +170,15 @@ _REF32 = {}
 def _ref32_on_host(key, sd, nf, params, w, T, seed):
     """The reference's fp32 sampler (oracle/ref_cpu.py, torch CPU fp32) on this host: final x and all snapshots."""
     if key not in _REF32:
-        torch.set_num_threads(min(16, max(1, len(os.sched_getaffinity(0)))))
-        fn = R.make_model_fn(R.clone_sd(sd), n_feat=nf, n_cfeat=6, height=64)
-        torch.manual_seed(seed)
-        with torch.no_grad():
-            x, inter = R.sample_ddpm(fn, 2, 64, params, w, T, _parity.golden_schedule(T), 6)
+        nthreads = torch.get_num_threads()
+        try:
+            torch.set_num_threads(min(16, max(1, len(os.sched_getaffinity(0)))))
+            fn = R.make_model_fn(R.clone_sd(sd), n_feat=nf, n_cfeat=6, height=64)
+            torch.manual_seed(seed)
+            with torch.no_grad():
+                x, inter = R.sample_ddpm(fn, 2, 64, params, w, T, _parity.golden_schedule(T), 6)
+        finally:
+            torch.set_num_threads(nthreads)
         _REF32[key] = (x.numpy(), np.asarray(inter))
     return _REF32[key]
 

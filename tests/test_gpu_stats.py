@@ -123,3 +123,18 @@ def test_pdfs_edges_and_ranges_vs_numpy():
     for b in range(5):
         ref = np.histogram(x[b].numpy().ravel(), edges, density=True)[0]
         _close(got[b], ref)
+
+
+@pytest.mark.parametrize("shape", [(32, 32), (16, 20, 24), (24, 40)])
+def test_power_spectrum_fp64_box(shape):
+    """a float64 box (values not representable in fp32) keeps fp64 input, as np.fft.fftn computes on it
+    (diffusion_utilities.py:322): HIP vs the fp64 oracle at the fp64 bar; a CUDA tensor input is used on its device."""
+    import cdm_amd
+    box = np.random.default_rng(7).standard_normal(shape) * (1 + 1e-9)
+    assert not np.array_equal(box.astype(np.float32).astype(np.float64), box)
+    k, pk = cdm_amd.power_spectrum(box, 0.5)
+    kr, pr = S.power_spectrum(box, 0.5)
+    np.testing.assert_array_equal(k, kr)
+    _close(pk, pr)
+    k2, pk2 = cdm_amd.power_spectrum(torch.from_numpy(box).cuda(), 0.5)
+    np.testing.assert_array_equal(pk2, pk)
