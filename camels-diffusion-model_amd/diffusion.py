@@ -42,11 +42,28 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+def sqrt_scalar_f32(v: torch.Tensor) -> torch.Tensor:
+    """fp32 sqrt of every element as a 0-d tensor op computes it: IEEE correctly rounded, the same on every host
+    (round(sqrt_fp64(x)) equals the correctly rounded fp32 sqrt: 53 >= 2 * 24 + 2 bits)."""
+    return torch.from_numpy(np.sqrt(v.detach().cpu().double().numpy()).astype(np.float32))
+
+
 class Schedule:
     """b_t, a_t, ab_t (T+1) computed with the reference's fp32 expressions on the host, plus the
-    per-step coefficient tables the kernels read (same fp32 operations as the reference)."""
+    per-step coefficient tables the kernels read (same fp32 operations as the reference).
 
-    def __init__(self, timesteps: int, device="cuda", beta1: float = BETA1, beta2: float = BETA2, tensors=None):
+    The reference's denoise_add_noise (code/train_diffusion_condition.py:274-279) takes sqrt in two forms: of the whole
+    vector, ``b_t.sqrt()[t]``, and of indexed 0-d scalars, ``a_t[t].sqrt()`` and ``(1 - ab_t[t]).sqrt()``.  torch's
+    vectorised CPU sqrt is not correctly rounded and differs between hosts in a few entries (round 5: the MI355X box's
+    host and the container that made the golden trajectories disagree in ``sqrt(b_t)``, ``sqrt(a_t)`` and
+    ``sqrt(1 - ab_t)``, tools/traj_diag.py, profiles/r5_traj_diag.json), while the 0-d form is IEEE everywhere.  So the
+    scalar forms are built with :func:`sqrt_scalar_f32` (host-independent, equal to the reference's values on any host)
+    and the vector forms (``sqrt(b_t)`` here, ``sqrt(ab_t)`` of perturb_input, :202-203) with torch's vector sqrt on
+    this host, as the reference evaluates them; ``sb`` replaces the latter with a given table (the trajectory parity
+    tests pass the golden host's, tests/golden/schedule.npz)."""
+
+    def __init__(self, timesteps: int, device="cuda", beta1: float = BETA1, beta2: float = BETA2, tensors=None,
+                 sb: Optional[torch.Tensor] = None):
         """``tensors=(b_t, a_t, ab_t)`` uses a caller's schedule (the functional sampler of
         code/sample_power_spectra.py:71-110 takes them as arguments) instead of building the default one."""
         self.T = int(timesteps)
@@ -61,11 +78,20 @@ class Schedule:
             ab_t[0] = 1
         dev = torch.device(device)
         self.b_t, self.a_t, self.ab_t = b_t.to(dev), a_t.to(dev), ab_t.to(dev)
-        self.sab = ab_t.sqrt().to(dev)                       # perturb: sqrt(ab[t])
+        self.sab = ab_t.sqrt().to(dev)                       # perturb: ab_t.sqrt()[t] (vector form)
         self.omab = (1 - ab_t).to(dev)                       #          (1 - ab[t])
-        self.coef = ((1 - a_t) / (1 - ab_t).sqrt()).to(dev)  # denoise: (1-a)/sqrt(1-ab)
-        self.sa = a_t.sqrt().to(dev)
-        self.sb = b_t.sqrt().to(dev)
+        # denoise: (1 - a_t[t]) / (1 - ab_t[t]).sqrt() and a_t[t].sqrt() (0-d forms), b_t.sqrt()[t] (vector form);
+        # fp32 subtraction / division in numpy: IEEE like torch's
+        oma = (1 - a_t).numpy()
+        self.coef = torch.from_numpy((oma / sqrt_scalar_f32(1 - ab_t).numpy()).astype(np.float32)).to(dev)
+        self.sa = sqrt_scalar_f32(a_t).to(dev)
+        if sb is not None:
+            sb = torch.as_tensor(sb).detach().to("cpu", torch.float32).reshape(-1)
+            if sb.numel() != self.T + 1:
+                raise ValueError(f"sb must have timesteps + 1 = {self.T + 1} entries")
+            self.sb = sb.to(dev)
+        else:
+            self.sb = b_t.sqrt().to(dev)
 
     def tensors(self):
         return self.b_t, self.a_t, self.ab_t
@@ -262,9 +288,10 @@ class DDPM:
     """Script-globals bundle of the reference (nn_model, timesteps, b_t/a_t/ab_t, n_cfeat, device)."""
 
     def __init__(self, model, timesteps: int, device="cuda", z_source: str = "device", seed: int = 1234,
-                 sched_tensors=None):
+                 sched_tensors=None, sched_sb=None):
+        """sched_tensors = (b_t, a_t, ab_t) and sched_sb = the b_t.sqrt() table to use (Schedule); None: built here."""
         self.model, self.T = model, int(timesteps)
-        self.sched = Schedule(self.T, device, tensors=sched_tensors)
+        self.sched = Schedule(self.T, device, tensors=sched_tensors, sb=sched_sb)
         self.b_t, self.a_t, self.ab_t = self.sched.tensors()
         self.device = torch.device(device)
         self.n_cfeat = model.n_cfeat

@@ -33,6 +33,15 @@ def golden_schedule(T: int):
     return tuple(torch.from_numpy(fx[f"{k}_{T}"].copy()) for k in ("b_t", "a_t", "ab_t"))
 
 
+def golden_sqrt_b(T: int):
+    """b_t.sqrt() as the golden host's torch evaluated it (tests/golden/add_sqrt_tables_r5.py): the vector-sqrt table
+    the reference's denoise_add_noise consumed when the golden trajectories were made (diffusion.Schedule(sb=...))."""
+    import numpy as np
+    import torch
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "schedule.npz"))
+    return torch.from_numpy(fx[f"sb_{T}"].copy())
+
+
 def record(name: str, **values):
     path = os.environ.get("CDM_PARITY_OUT")
     if not path:

@@ -2,9 +2,13 @@
 d loss / d x (the image), d loss / d t and d loss / d c, with per-sample and with broadcast t / c (one row, the shapes
 code/diffusion_utilities.py:137-145 views to [-1, in_dim]), against torch autograd of the CPU oracle.
 
-Tolerance: relative L2 of each input gradient and of every parameter gradient vs an fp64 autograd run of the oracle, at
-most 3x the reference's own fp32 deviation from that fp64 run plus a floor of 2e-6 (the fp32 rounding of a gradient the
-network barely amplifies).  Train-mode BatchNorm, n_feat = 16, B = 4, on an input where no arithmetic flips a kink.
+Tolerance (_branch_check): relative L2 of each input gradient and of every parameter gradient vs an fp64 autograd run
+of the oracle on the same branch of the piecewise-linear network (HIP's own ReLU / MaxPool decisions imposed), at most 3x
+the reference's own fp32 deviation from fp64 on ITS branch plus a floor of 2e-6 (the fp32 rounding of a gradient the
+network barely amplifies).  Train-mode BatchNorm, n_feat = 16, B = 4, input seeds 0..2 (round 4 selected a seed on which
+no arithmetic flips a decision; round 5's audit, tools/kink_diag.py / profiles/r5_kink_diag.txt, found HIP's per-layer
+pre-activation errors equal to or below the reference's on every layer — the flips are single elements at |z| below
+the rounding error, which either arithmetic takes by chance, and the strict bar per branch needs no seed selection).
 """
 import numpy as np
 import pytest
@@ -30,8 +34,55 @@ def _rel_l2(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
 
 
-def _oracle(sd, x, t, c, sc, dtype, weight, train=True):
-    """autograd of the oracle forward (train / eval BatchNorm) -> (eps, dx, dt, dc, param grads)."""
+class _Kinks:
+    """The oracle's ReLU / MaxPool decisions (torch.nn.functional calls of oracle/ref_cpu.py's forward, in call order):
+    capture=True records them (relu: mask z > 0 and z; max_pool2d(2): the first-max index of each 2x2 window, the
+    order of torch's CPU kernel); otherwise the given decisions are imposed — relu(z) = z * mask, the pool output taken
+    at the given index — so autograd runs the backward of THAT branch of the piecewise-linear network."""
+
+    def __init__(self, relu=None, pool=None):
+        self.capture = relu is None
+        self.relu, self.pool = ([], []) if self.capture else (list(relu), list(pool))
+
+    def __enter__(self):
+        self._relu, self._pool = R.F.relu, R.F.max_pool2d
+        it_r, it_p = iter(self.relu), iter(self.pool)
+
+        def relu(z, inplace=False):
+            if self.capture:
+                self.relu.append(((z > 0).detach().clone(), z.detach().clone()))
+                return self._relu(z)
+            return z * next(it_r)[0].to(z.dtype)
+
+        def pool(v, k, *a, **kw):
+            B, C, H, W = v.shape
+            win = v.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+            if self.capture:
+                self.pool.append(_first_max(win.detach()))
+                return self._pool(v, k, *a, **kw)
+            return win.gather(-1, next(it_p).unsqueeze(-1)).squeeze(-1)
+        R.F.relu, R.F.max_pool2d = relu, pool
+        return self
+
+    def __exit__(self, *exc):
+        R.F.relu, R.F.max_pool2d = self._relu, self._pool
+
+
+def _first_max(win):
+    """index of the first maximum over the last axis (NaN wins, as torch's CPU max_pool2d and the HIP pool apply)"""
+    best = win[..., 0].clone()
+    arg = torch.zeros(best.shape, dtype=torch.int64)
+    for e in range(1, win.shape[-1]):
+        v = win[..., e]
+        take = (v > best) | torch.isnan(v)
+        best = torch.where(take, v, best)
+        arg = torch.where(take, torch.full_like(arg, e), arg)
+    return arg
+
+
+def _oracle(sd, x, t, c, sc, dtype, weight, train=True, kinks=None):
+    """autograd of the oracle forward (train / eval BatchNorm) -> (eps, dx, dt, dc, param grads); kinks: a _Kinks
+    context (capture or impose)"""
     sd = {k: (v.to(dtype) if v.is_floating_point() else v.clone()).clone() for k, v in sd.items()}
     keys = [k for k, _, kind in R.state_dict_layout(1, NF, NCF, H) if kind == "param"]
     for k in keys:
@@ -39,27 +90,115 @@ def _oracle(sd, x, t, c, sc, dtype, weight, train=True):
     xx = x.to(dtype).clone().requires_grad_(True)
     tt = t.to(dtype).clone().requires_grad_(True)
     cc = c.to(dtype).clone().requires_grad_(True)
-    eps = R.unet_forward(sd, xx, tt, cc, n_feat=NF, n_cfeat=NCF, height=H, train=train,
-                         shortcut=(sc[0].to(dtype), sc[1].to(dtype)))
+    import contextlib
+    with (kinks if kinks is not None else contextlib.nullcontext()):
+        eps = R.unet_forward(sd, xx, tt, cc, n_feat=NF, n_cfeat=NCF, height=H, train=train,
+                             shortcut=(sc[0].to(dtype), sc[1].to(dtype)))
     (eps * weight.to(dtype)).sum().backward()
     return eps.detach(), xx.grad, tt.grad, cc.grad, {k: sd[k].grad for k in keys}
 
 
-# inputs of test_input_grads_vs_autograd: chosen by tools/input_grad_seed_scan.py on the GPU box (profiles/
-# r4_input_grad_seed_scan.txt) so that no arithmetic flips a ReLU / MaxPool kink — with train-mode BatchNorm over 4
-# images, 8 of the first 10 seeds flip one under fp32 or h3 (the reference's own fp32 run flips none against fp64), and
-# a flipped kink reroutes a gradient (relative L2 1e-3 .. 2e-2).  The strict bar then holds for every tensor.
-KINK_FREE_SEED = 2
+def _hip_kinks(m, x, t, c, sc, frozen):
+    """HIP's decisions in the oracle's call order, from one engine forward on the same inputs (deterministic, the
+    kernels of the module call): per ReLU the mask of z = fma(y, s, t) > 0 (NCHW) and z, per MaxPool the first-max index
+    of relu(z) over each window (the pool apply's order).  Call order: the 10 encoder Conv-BN-ReLU layers (a pool after
+    the 6th and the 10th), up0's GroupNorm-ReLU, the 8 decoder layers, out.1's GroupNorm-ReLU."""
+    eng, P = m._engine_and_params()
+    s = torch.cuda.current_stream().cuda_stream
+    eng.repack(P, True, s)
+    ws = eng.workspace(B, True, frozen=frozen)
+    eng.forward(ws, P, x.cuda().reshape(B, H, H), t.cuda(), c.cuda(), sc[0].reshape(-1).cuda(), sc[1].cuda(), B, s,
+                frozen=frozen)
+    torch.cuda.synchronize()
+
+    def z_of(y, scale, shift, C, S, per_sample):
+        y = y.double().cpu().reshape(B, S, S, C)
+        sc_ = scale.double().cpu().reshape(B if per_sample else 1, 1, 1, C)
+        sh = shift.double().cpu().reshape(B if per_sample else 1, 1, 1, C)
+        z = (y * sc_ + sh).float().permute(0, 3, 1, 2).contiguous()
+        return z
+
+    relu, pool = [], []
+    L = eng.layers
+    for i, l in enumerate(L):
+        st = ws.bn[l.name]
+        z = z_of(ws.y[l.name], st["scale"], st["shift"], l.cout, l.S, False)
+        relu.append((z > 0, z))
+        if l.name in ("down1.model.1.conv2", "down2.model.1.conv2"):
+            Bz, C, S, _ = z.shape
+            r = torch.relu(z)
+            win = r.reshape(Bz, C, S // 2, 2, S // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(Bz, C, S // 2, S // 2, 4)
+            pool.append(_first_max(win))
+        if i == 9:
+            z0 = z_of(ws.y0, ws.gn0["scale"], ws.gn0["shift"], 2 * NF, H // 4, True)
+            relu.append((z0 > 0, z0))
+    zO = z_of(ws.yO, ws.gnO["scale"], ws.gnO["shift"], NF, H, True)
+    relu.append((zO > 0, zO))
+    return relu, pool
 
 
+def _branch_check(tag, m, sd, inputs, hip_grads, train, rec):
+    """HIP's gradients vs fp64 autograd of the oracle on HIP's own branch (its ReLU / MaxPool decisions imposed) and the
+    reference's fp32 gradients vs fp64 on the reference's branch: a ReLU / MaxPool decision at |z| of the rounding error
+    is a discrete choice either arithmetic may make (both are exact gradients of their branch); the bar compares the
+    arithmetic error of each on its own branch — every tensor within 3x the reference's + 2e-6.  Also held: HIP's
+    per-layer pre-activation error within 3x the reference's, and the decisions each arithmetic flips relative to fp64
+    are counted (recorded)."""
+    x, t, c, sc, weight = inputs
+    cap64, cap32 = _Kinks(), _Kinks()
+    _oracle(sd, x, t, c, sc, torch.float64, weight, train, cap64)
+    e32, dx32, dt32, dc32, g32 = _oracle(sd, x, t, c, sc, torch.float32, weight, train, cap32)
+    hk_relu, hk_pool = _hip_kinks(m, x, t, c, sc, frozen=not train)
+    assert len(hk_relu) == len(cap64.relu) == 20 and len(hk_pool) == len(cap64.pool) == 2
+    e64h, dx64h, dt64h, dc64h, g64h = _oracle(sd, x, t, c, sc, torch.float64, weight, train, _Kinks(hk_relu, hk_pool))
+    e64r, dx64r, dt64r, dc64r, g64r = _oracle(sd, x, t, c, sc, torch.float64, weight, train,
+                                              _Kinks(cap32.relu, cap32.pool))
+    flips_h = sum(int((a[0] != b[0]).sum()) for a, b in zip(hk_relu, cap64.relu)) + \
+        sum(int((a != b).sum()) for a, b in zip(hk_pool, cap64.pool))
+    flips_r = sum(int((a[0] != b[0]).sum()) for a, b in zip(cap32.relu, cap64.relu)) + \
+        sum(int((a != b).sum()) for a, b in zip(cap32.pool, cap64.pool))
+    zbad = []
+    for j, ((_, zh), (_, zr), (_, z64)) in enumerate(zip(hk_relu, cap32.relu, cap64.relu)):
+        z64 = z64.double(); scale = z64.abs().max().item()
+        eh = (zh.double() - z64).abs().max().item() / scale
+        er = (zr.double() - z64).abs().max().item() / scale
+        if eh > 3 * er + 1e-7:
+            zbad.append((j, eh, er))
+    hip_eps, hip_dx, hip_dt, hip_dc, hip_p = hip_grads
+    bad = []
+    if _rel_l2(hip_eps, e64h) > 3 * _rel_l2(e32, e64r) + 2e-6:
+        bad.append(("eps", _rel_l2(hip_eps, e64h), _rel_l2(e32, e64r)))
+    items = [("x", hip_dx, dx64h, dx32, dx64r), ("t", hip_dt, dt64h, dt32, dt64r), ("c", hip_dc, dc64h, dc32, dc64r)]
+    items += [(k, hip_p[k], g64h[k], g32[k], g64r[k]) for k in g64h]
+    worst = 0.0
+    for name, hip, r64h, r32, r64r in items:
+        assert hip is not None and tuple(hip.shape) == tuple(r64h.shape), name
+        if r64h.norm() == 0 and r64r.norm() == 0:
+            continue
+        eh, er = _rel_l2(hip, r64h), _rel_l2(r32, r64r)
+        rec[name] = (eh, er)
+        worst = max(worst, eh / (3 * er + 2e-6))
+        if eh > 3 * er + 2e-6:
+            bad.append((name, eh, er))
+    print(f"[{tag}] decisions flipped vs fp64: HIP {flips_h}, reference fp32 {flips_r}; worst ratio {worst:.2f}; "
+          f"worst", sorted(rec.items(), key=lambda kv: -kv[1][0])[:3])
+    _parity.record("input_grads_branch", tag=tag, flips_hip=flips_h, flips_ref32=flips_r, worst_ratio=worst,
+                   layers_z_over=zbad, errors={k: {"hip": a, "ref32": b} for k, (a, b) in rec.items()})
+    assert not zbad, zbad
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
 @pytest.mark.parametrize("math", ["fp32", "h3"])
 @pytest.mark.parametrize("bcast", [False, True])
-def test_input_grads_vs_autograd(math, bcast):
+def test_input_grads_vs_autograd(math, bcast, seed):
+    """dx, dt, dc and every parameter gradient (train-mode BatchNorm, n_feat 16, B 4) vs fp64 autograd of the oracle,
+    on the first three input seeds of tools/input_grad_seed_scan.py (no seed selection): _branch_check."""
     import cdm_amd
-    torch.manual_seed(3 + 100 * KINK_FREE_SEED)
+    torch.manual_seed(3 + 100 * seed)
     m = cdm_amd.ContextUnet(1, NF, NCF, H, conv_math=math).cuda().train()
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
-    g = torch.Generator().manual_seed(11 + 100 * KINK_FREE_SEED)
+    g = torch.Generator().manual_seed(11 + 100 * seed)
     x = torch.randn(B, 1, H, H, generator=g)
     rows = 1 if bcast else B
     t = torch.rand(rows, generator=g)
@@ -71,28 +210,13 @@ def test_input_grads_vs_autograd(math, bcast):
     torch.manual_seed(21)
     eps = m(xg, tg, cg)
     (eps * weight.cuda()).sum().backward()
-    e64, dx64, dt64, dc64, g64 = _oracle(sd, x, t, c, sc, torch.float64, weight)
-    e32, dx32, dt32, dc32, g32 = _oracle(sd, x, t, c, sc, torch.float32, weight)
-    assert _rel_l2(eps.detach(), e64) <= 3 * _rel_l2(e32, e64) + 2e-6
-    rec, bad = {}, []
-    for name, hip, r64, r32 in (("x", xg.grad.view(B, 1, H, H), dx64, dx32), ("t", tg.grad, dt64, dt32),
-                                ("c", cg.grad, dc64, dc32)):
-        assert hip is not None and tuple(hip.shape) == tuple(r64.shape), name
-        eh, er = _rel_l2(hip, r64), _rel_l2(r32, r64)
-        rec[name] = (eh, er)
-        if eh > 3 * er + 2e-6:
-            bad.append(f"d/d{name}: HIP {eh:.3e} vs reference fp32 {er:.3e}")
-    worst = 0.0
-    for k, p in m.named_parameters():            # broadcast: the embedding gradients summed over the batch
-        eh, er = _rel_l2(p.grad, g64[k]), _rel_l2(g32[k], g64[k])
-        worst = max(worst, eh / (3 * er + 2e-6))
-        rec[k] = (eh, er)
-        if eh > 3 * er + 2e-6:
-            bad.append(f"{k}: HIP {eh:.3e} vs reference fp32 {er:.3e}")
-    print({k: f"{a:.2e}/{b:.2e}" for k, (a, b) in rec.items()})
-    _parity.record("input_grads", conv_math=math, broadcast=bcast,
-                   errors={k: {"hip": a, "ref32": b} for k, (a, b) in rec.items()}, worst_param_ratio=worst)
-    assert not bad, bad
+    hip = (eps.detach(), xg.grad.view(B, 1, H, H), tg.grad, cg.grad, {k: p.grad for k, p in m.named_parameters()})
+    sd_after = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    # the engine forward of _hip_kinks runs on the state before the module call (train mode: batch statistics; the
+    # running statistics it updates again are not read)
+    m.load_state_dict(sd)
+    _branch_check(f"{math}/{'b' if bcast else 's'}/seed{seed}", m, sd, (x, t, c, sc, weight), hip, True, {})
+    m.load_state_dict(sd_after)
 
 
 @pytest.mark.parametrize("fused", [True, False])
@@ -195,16 +319,17 @@ def test_two_models_interleaved_backward():
         assert torch.equal(grads[0][k], grads[1][k]), k
 
 
+@pytest.mark.parametrize("seed", [0, 1])
 @pytest.mark.parametrize("math", ["fp32", "h3"])
-def test_eval_mode_grads_vs_autograd(math):
+def test_eval_mode_grads_vs_autograd(math, seed):
     """Gradients through model.eval() (BatchNorm on the running statistics, batch_norm(training=False) under autograd:
     dy = gamma invstd g_pre, no batch terms), input and parameter gradients, against the oracle's autograd in eval mode
-    (fp64 truth, same bar as test_input_grads_vs_autograd).  Running statistics made non-trivial by two train forwards
+    (_branch_check, as test_input_grads_vs_autograd).  Running statistics made non-trivial by two train forwards
     first; they must not move during the eval forward / backward."""
     import cdm_amd
-    torch.manual_seed(3 + 100 * KINK_FREE_SEED)
+    torch.manual_seed(3 + 100 * seed)
     m = cdm_amd.ContextUnet(1, NF, NCF, H, conv_math=math).cuda().train()
-    g = torch.Generator().manual_seed(11 + 100 * KINK_FREE_SEED)
+    g = torch.Generator().manual_seed(11 + 100 * seed)
     with torch.no_grad():
         for _ in range(2):
             m(torch.randn(B, 1, H, H, generator=g).cuda(), torch.rand(B, generator=g).cuda(),
@@ -224,21 +349,5 @@ def test_eval_mode_grads_vs_autograd(math):
     for k, v in m.state_dict().items():
         if "running" in k or "num_batches" in k:
             assert torch.equal(v.cpu(), sd[k]), k
-    e64, dx64, dt64, dc64, g64 = _oracle(sd, x, t, c, sc, torch.float64, weight, train=False)
-    e32, dx32, dt32, dc32, g32 = _oracle(sd, x, t, c, sc, torch.float32, weight, train=False)
-    assert _rel_l2(eps.detach(), e64) <= 3 * _rel_l2(e32, e64) + 2e-6
-    rec, bad = {}, []
-    hip_p = dict(m.named_parameters())
-    items = [("x", xg.grad.view(B, 1, H, H), dx64, dx32), ("t", tg.grad, dt64, dt32), ("c", cg.grad, dc64, dc32)]
-    items += [(k, hip_p[k].grad, g64[k], g32[k]) for k in g64]
-    for name, hip, r64, r32 in items:
-        assert hip is not None, name
-        if r64.norm() == 0:
-            continue
-        eh, er = _rel_l2(hip, r64), _rel_l2(r32, r64)
-        rec[name] = (eh, er)
-        if eh > 3 * er + 2e-6:
-            bad.append((name, eh, er))
-    _parity.record("eval_mode_grads", conv_math=math, worst=sorted(rec.items(), key=lambda kv: -kv[1][0])[:5])
-    print(f"[{math}] eval-mode gradients: worst", sorted(rec.items(), key=lambda kv: -kv[1][0])[:4])
-    assert not bad, bad
+    hip = (eps.detach(), xg.grad.view(B, 1, H, H), tg.grad, cg.grad, {k: p.grad for k, p in m.named_parameters()})
+    _branch_check(f"eval/{math}/seed{seed}", m, sd, (x, t, c, sc, weight), hip, False, {})
