@@ -14,7 +14,7 @@ kernels the engine uses for the same layers: BatchNorm / ReLU / MaxPool backward
 (`cdm_norm_bwd_reduce`, `cdm_bn_bwd_finalize`, `cdm_norm_apply_bwd`), conv weight gradients (`cdm_conv3x3_wgrad`, the
 C_in = 1 form `cdm_conv3x3_cin1_wgrad`), input gradients (the conv on the flipped weights), ConvTranspose backward
 (`cdm_convT2x2_wgrad / dgrad`), EmbedFC backward (`cdm_embed_bwd`).  Parameter gradients always; the input gradient
-of every input (EmbedFC: input_dim % 4 == 0), incl. the C_in = 1 image of a ResidualConvBlock(1, C) (the flipped-weight
+of every input (EmbedFC: any input_dim), incl. the C_in = 1 image of a ResidualConvBlock(1, C) (the flipped-weight
 conv `cdm_conv3x3_cin1_dgrad`, plus the random 1x1 shortcut's sum_c w[c] g[c] for is_res).  Eval-mode calls under
 autograd run the same taped form with BatchNorm frozen on the running statistics (`cdm_bn_fwd_frozen`, backward
 `cdm_bn_bwd_finalize_frozen`: the backward of batch_norm(training=False)), as ContextUnet's.
@@ -433,7 +433,7 @@ def _input_grad(tape: "_Tape", g, need, shapes):
 def embed_fc_forward(mod, x: torch.Tensor) -> torch.Tensor:
     """EmbedFC.forward (diffusion_utilities.py:137-145): x.view(-1, input_dim) -> Linear -> GELU -> Linear; with
     gradients: cdm_embed_bwd (the engine's EmbedFC backward) on the saved pre-activation and activation, the input
-    gradient dpre . W1 by cdm_gemm_f32 (input_dim % 4 == 0)."""
+    gradient dpre . W1 by cdm_embed_input_grad (any input_dim)."""
     dev = next(mod.parameters()).device
     x0 = x
     x = _check(x.to(dev), "EmbedFC").reshape(-1, mod.input_dim).contiguous()
@@ -483,11 +483,10 @@ def embed_fc_forward(mod, x: torch.Tensor) -> torch.Tensor:
             tape.add(p_, g_)
         if not need[0]:
             return [None]
-        if in_dim % 4:
-            raise NotImplementedError("the EmbedFC input gradient on the HIP path needs input_dim % 4 == 0")
+        # dx = dpre . W1 for any input_dim (the reference's context embeddings take n_cfeat = 5 or 6): the kernel
+        # ContextUnet's dt / dc use, with the second MLP empty
         dx = torch.empty(rows, in_dim, device=dev)
-        lib().cdm_gemm_f32(dpre.data_ptr(), E, rows, E, w1.data_ptr(), in_dim, in_dim, dx.data_ptr(), in_dim, None, 1,
-                           0, 1, None, _s())
+        lib().cdm_embed_input_grad(dpre.data_ptr(), w1.data_ptr(), E, None, None, 0, rows, in_dim, dx.data_ptr(), _s())
         return [dx.reshape(shapes[0])]
     tape.backward = backward
     return _finish(out, mod, tape, (x0,))

@@ -180,9 +180,23 @@ struct LdConvT2x2GatherB {  // convT 2x2 wgrad: B(k = input pix (n,h,w), n = ij*
 
 enum { EPI_RELU = 1, EPI_ACCUM = 2 };
 
+// Eval-mode output transforms fused into the conv epilogue (EpiStoreW<..., FUSE = true>; the norm_apply_fwd forms of
+// diffusion_utilities.py:54-55 / :109 and ContextUnet.py:57-58 after a BatchNorm folded into the weights), applied to
+// v = relu(acc + bias):
+//   RESID  out = w[c] x[pix] + b[c] + v  (the random 1x1 shortcut of the C_in = 1 image; set 1 for images >= split)
+//   FILM   out = a[img][c] v + b[img][c]
+//   POOL   out[pooled pixel] = max over the 2x2 window (MaxPool2d(2): NaN wins), image width 32 or 64
+enum { FUSE_RESID = 1, FUSE_FILM = 2, FUSE_POOL = 3 };
+struct EpiFuse {
+    int kind = 0;
+    int hw = 1, W = 1;                      // pixels per image and image width of the conv's output grid
+    const float* x = nullptr; const float* w = nullptr; const float* b = nullptr; int split = 0;   // RESID
+    const float* fa = nullptr; int fan = 0; const float* fb = nullptr; int fbn = 0;                 // FILM
+};
+
 // WM = waves along M (2: 128-row block, 4: 256-row block); stats per 128-row tile.  OT = the stored element type (bf16:
 // C4's fused-chain activations and gradients; the statistics / maxima are those of the stored, rounded values)
-template <int WM = 2, class OT = float, bool ACC = false>
+template <int WM = 2, class OT = float, bool ACC = false, bool FUSE = false>
 struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-tile column stats
     OT* y; long long ldy; long long zstride; const float* bias; int bias_mod; int flags;
     float* stats; int stats_ld;  // stats[tile][0|1][stats_ld]: sum / sum of squares of the stored value
@@ -190,8 +204,89 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
     float* amax = nullptr;       // optional running max|stored value| (block_amax_commit)
     int* ymm = nullptr;          // optional per-column max / min of the stored value, ordered-int keys (fkey):
     int ymm_ld = 0;              //   ymm[n] (atomic max), ymm[ymm_ld + n] (atomic min); needs stats
+    EpiFuse fz{};                // FUSE: the eval-mode output transform (LDS-halo conv, whole 256-pixel tiles)
+
+    // FUSE (eval forward, conv3x3_halo_x3_kernel): relu(acc + bias), then fz's transform; the whole block tile is in
+    // range (host: M % 256 == 0, N % 128 == 0) and a 256-pixel tile lies in one image (hw % 256 == 0).  POOL: at
+    // W = 32 a wave's two row blocks are two image rows (the 2x2 window is in registers); at W = 64 a wave holds one
+    // image row and its vertical neighbour is wave wm ^ 1 (exchanged through scratch, 16 KiB per round, two rounds).
+    __device__ __forceinline__ void fused(f32x16 (&acc)[2][2], int mw, int nw, int lane, int wm, int wn,
+                                          float* scratch) const {
+        const int img = mw / fz.hw;
+        float bj[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bj[j] = bias ? bias[nw + 32 * j + (lane & 31)] : 0.f;
+        float am = 0.f;
+        if (fz.kind == FUSE_POOL) {
+            float hp[2][2][8];   // horizontal pairs (rows r, r + 1 of an accumulator: pixels d, d + 1)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const float a = relu_f(acc[i][j][2 * k] + bj[j]), b = relu_f(acc[i][j][2 * k + 1] + bj[j]);
+                        hp[i][j][k] = (b > a || isnan(b)) ? b : a;
+                        am = fmaxf(am, hp[i][j][k]);
+                    }
+            const int hw4 = fz.hw >> 2, Wo = fz.W >> 1;
+            auto put = [&](int i, int j, int k, float v) {   // pooled value of the window at accumulator (i, j, 2k)
+                const int m = mw + 32 * i + (2 * k & 3) + 8 * (2 * k >> 2) + 4 * (lane >> 5);
+                const int p = m - img * fz.hw, h = p / fz.W, c = p - h * fz.W;
+                const long long o = (long long)img * hw4 + (h >> 1) * Wo + (c >> 1);
+                Act<OT>::store(y + o * ldy + nw + 32 * j + (lane & 31), Act<OT>::round(v));
+            };
+            if (fz.W == 32) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const float a = hp[0][j][k], b = hp[1][j][k];
+                        put(0, j, k, (b > a || isnan(b)) ? b : a);
+                    }
+            } else {
+                float* xs = scratch + ((wm >> 1) * 2 + wn) * 16 * 64;   // [pair][wn][16 values][64 lanes]
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    if (wm & 1) {
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) xs[(j * 8 + k) * 64 + lane] = hp[i][j][k];
+                    }
+                    __syncthreads();
+                    if (!(wm & 1)) {
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) {
+                                const float a = hp[i][j][k], b = xs[(j * 8 + k) * 64 + lane];
+                                put(i, j, k, (b > a || isnan(b)) ? b : a);
+                            }
+                    }
+                    __syncthreads();
+                }
+            }
+        } else {
+            const int sel = img >= fz.split ? N : 0;
+            CDM_FOR_ACC({
+                float v = relu_f(acc[i][j][r] + bj[j]);
+                if (fz.kind == FUSE_RESID) v = fmaf(fz.w[sel + n], fz.x[m], fz.b[sel + n]) + v;
+                else v = fmaf(fz.fa[img * fz.fan + n], v, fz.fb[img * fz.fbn + n]);
+                v = Act<OT>::round(v);
+                Act<OT>::store(y + (long long)m * ldy + n, v);
+                am = fmaxf(am, fabsf(v));
+            })
+        }
+        if (amax) block_amax_commit(am, amax);
+    }
+
     __device__ __forceinline__ void operator()(f32x16 (&acc)[2][2], int mw, int nw, int lane, int wm, int wn,
                                                float* scratch, int tid) const {
+        if constexpr (FUSE) {
+            fused(acc, mw, nw, lane, wm, wn, scratch);
+            return;
+        }
         OT* yz = y + (long long)blockIdx.z * zstride;      // 0 when the kernel applied its own (remapped) slab
         float cs[2] = {0.f, 0.f}, cq[2] = {0.f, 0.f};
         float cmx[2] = {-INFINITY, -INFINITY}, cmn[2] = {INFINITY, INFINITY};
@@ -434,7 +529,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
 };
 using EpiStore = EpiStoreW<2>;
 template <class EP> struct IsEpiStoreW : std::false_type {};
-template <int WM, class OT, bool ACC> struct IsEpiStoreW<EpiStoreW<WM, OT, ACC>> : std::true_type {};
+template <int WM, class OT, bool ACC, bool FUSE> struct IsEpiStoreW<EpiStoreW<WM, OT, ACC, FUSE>> : std::true_type {};
 
 struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n, 2h+i, 2w+j, co] = acc + b[co]
     float* y; long long ldy; const float* bias; int H, W, Co, M, N;
@@ -2075,11 +2170,11 @@ static int halo_deep() {
 
 // XT / OT: element types of the source (x, PRE's y) and of the stored output; bf16 only with the one-term (C4)
 // arithmetic
-template <int WT, class PRE = PreNone, class XT = float, class OT = float, bool ACC = false>
+template <int WT, class PRE = PreNone, class XT = float, class OT = float, bool ACC = false, bool FUSE = false>
 static int launch_conv_halo(const XT* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
-                            const float* amax_x, const float* amax_w, const EpiStoreW<4, OT, ACC>& ep, int nterm,
+                            const float* amax_x, const float* amax_w, const EpiStoreW<4, OT, ACC, FUSE>& ep, int nterm,
                             hipStream_t s, PRE pre = PRE{}, int tpb = 0) {
-    using EP = EpiStoreW<4, OT, ACC>;
+    using EP = EpiStoreW<4, OT, ACC, FUSE>;
     constexpr bool F32 = std::is_same<XT, float>::value && std::is_same<OT, float>::value;
     const int M = N * H * WT, mtiles = M / HBM_;
     // the kernel addresses the halo sources (x, pre.y) by 32-bit byte offsets from their base
@@ -2122,14 +2217,19 @@ static int launch_conv_halo(const XT* x, int N, int H, int Cin, int ldx, const _
             break;
         default:
             if constexpr (F32) {
-                switch (nterm) {
-                    case 3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<3, WT, EP, true, 1, PRE>), grid, dim3(HTHREADS), 0, s, x, H,
-                                               Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
-                    case NT_H3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EP, true, 1, PRE>), grid, dim3(HTHREADS), 0,
-                                                   s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
-                    case 6: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<6, WT, EP, true, 0, PRE>), grid, dim3(HTHREADS), 0, s, x, H,
-                                               Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
-                    default: return (int)hipErrorInvalidValue;
+                if (nterm == NT_H3) {
+                    hipLaunchKernelGGL((conv3x3_halo_x3_kernel<NT_H3, WT, EP, true, 1, PRE>), grid, dim3(HTHREADS), 0,
+                                       s, x, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm));
+                } else if constexpr (!FUSE) {   // the x3 / x6 arithmetics: no fused eval epilogue
+                    switch (nterm) {
+                        case 3: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<3, WT, EP, true, 1, PRE>), grid, dim3(HTHREADS), 0, s, x, H,
+                                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
+                        case 6: hipLaunchKernelGGL((conv3x3_halo_x3_kernel<6, WT, EP, true, 0, PRE>), grid, dim3(HTHREADS), 0, s, x, H,
+                                                   Cin, ldx, wx3, Cout, amax_x, amax_w, ep, pre, mtiles, tpb, halo_stagger(nterm)); break;
+                        default: return (int)hipErrorInvalidValue;
+                    }
+                } else {
+                    return (int)hipErrorInvalidValue;
                 }
             } else {
                 return (int)hipErrorInvalidValue;
@@ -2140,11 +2240,19 @@ static int launch_conv_halo(const XT* x, int N, int H, int Cin, int ldx, const _
 }
 
 // LDS-halo conv of a W x W image (W in {32, 64}; 128 / 256 with the h3 arithmetic only)
-template <class PRE = PreNone, class XT = float, class OT = float, bool ACC = false>
+template <class PRE = PreNone, class XT = float, class OT = float, bool ACC = false, bool FUSE = false>
 static int launch_conv_halo_w(int W, const XT* x, int N, int H, int Cin, int ldx, const __bf16* wx3, int Cout,
-                              const float* amax_x, const float* amax_w, const EpiStoreW<4, OT, ACC>& ep, int nterm,
+                              const float* amax_x, const float* amax_w, const EpiStoreW<4, OT, ACC, FUSE>& ep, int nterm,
                               hipStream_t s, PRE pre = PRE{}) {
-    if constexpr (ACC) {   // the accumulating (load-ahead epilogue) variant: the dgrads at 32^2 / 64^2 only
+    if constexpr (FUSE) {   // the fused eval epilogue: 32^2 / 64^2 maps (C2 / C4)
+        switch (W) {
+            case 32: return launch_conv_halo<32, PRE, XT, OT, ACC, FUSE>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep,
+                                                                         nterm, s, pre);
+            case 64: return launch_conv_halo<64, PRE, XT, OT, ACC, FUSE>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep,
+                                                                         nterm, s, pre);
+            default: return (int)hipErrorInvalidValue;
+        }
+    } else if constexpr (ACC) {   // the accumulating (load-ahead epilogue) variant: the dgrads at 32^2 / 64^2 only
         switch (W) {
             case 32: return launch_conv_halo<32, PRE, XT, OT, ACC>(x, N, H, Cin, ldx, wx3, Cout, amax_x, amax_w, ep, nterm,
                                                                    s, pre);

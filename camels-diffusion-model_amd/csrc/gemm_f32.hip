@@ -45,7 +45,7 @@ __global__ void split_f16x2_kernel(const float* __restrict__ b, long long ldb, i
 struct PackSplitJob {
     const float* W;          // OIHW [Cout][Cin][3][3]
     int Cin, Cout, kc;       // kc: K order (16 = channel-chunk-major, 0 = tap-major), as cdm_pack_conv3x3
-    int pad_;
+    int mode;                // 0: the h3 split (fp16 hi / lo of W * 2^(14 - e)), 1: one bf16 term (C4; plane 0 only)
     __bf16* wpk_x;           // fwd operand  [ceil(9 Cin / 16)][3][Cout][16]  (K = tap/ci, N = co)
     __bf16* wdg_x;           // dgrad operand [ceil(9 Cout / 16)][3][Cin][16] (K = tap'/co, N = ci), W flipped
     float* amax;             // max|W| (the split scale of both images)
@@ -69,7 +69,8 @@ __global__ __launch_bounds__(256) void pack_split_batch_kernel(const PackSplitJo
     __bf16* out = dg ? j.wdg_x : j.wpk_x;
     if (!out) return;
     const int K = 9 * (dg ? j.Cout : j.Cin), N = dg ? j.Cin : j.Cout;
-    const float sc = op_scale<NT_H3>(j.amax);
+    const bool one = j.mode == 1;
+    const float sc = one ? 1.f : op_scale<NT_H3>(j.amax);
     const int ktiles = (K + XBK - 1) / XBK;
     const long long total = (long long)ktiles * N * XBK;
     for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long long)gridDim.x * blockDim.x) {
@@ -82,9 +83,13 @@ __global__ __launch_bounds__(256) void pack_split_batch_kernel(const PackSplitJo
             if (!dg) { unk(k, j.Cin, j.kc, tap, c); v = j.W[((long long)n * j.Cin + c) * 9 + tap]; }          // W[co=n][ci=c]
             else     { unk(k, j.Cout, j.kc, tap, c); v = j.W[((long long)c * j.Cin + n) * 9 + (8 - tap)]; }  // W[co=c][ci=n]
         }
+        __bf16* o = out + (((long long)kt * 3) * N + n) * XBK + kk;
+        if (one) {          // the hi plane of cdm_split_bf16x3 (the one-term arithmetic reads no other)
+            o[0] = (__bf16)v;
+            continue;
+        }
         v *= sc;
         const _Float16 h = (_Float16)v;
-        __bf16* o = out + (((long long)kt * 3) * N + n) * XBK + kk;
         o[0] = __builtin_bit_cast(__bf16, h);
         o[(long long)N * XBK] = __builtin_bit_cast(__bf16, (_Float16)(v - (float)h));
     }
@@ -397,6 +402,20 @@ CDM_API int cdm_gemm_f32(const float* a, long long lda, int M, int K, const floa
 }
 
 CDM_API int cdm_gemm_splits(int K, int splits) { return effective_splits(K, splits); }
+
+// C[m][n] = A[m][k] . B[k][n] + bias[n % bias_mod] on the 16-bit matrix cores (nterm: NT_H3 or one bf16 term);
+// wx = the split image of B (cdm_split_f16x2 / cdm_split_bf16x3 of [K][N]); h3: max|A| = *amax_a, max|B| = *amax_w.
+// amax_c (optional): running max|C|.  up0's ConvTranspose2d(k = h/4) on the 1x1 map (ContextUnet.py:26-30).
+CDM_API int cdm_gemm_x16(const float* a, long long lda, int M, int K, const void* wx, const float* amax_a,
+                         const float* amax_w, int N, float* c, long long ldc, const float* bias, int bias_mod,
+                         float* amax_c, int nterm, void* stream) {
+    if (!x16_ok(nterm) || !x16_amax_ok(nterm, amax_a, amax_w) || K % 4 || N % 4 || lda % 4)
+        return (int)hipErrorInvalidValue;
+    EpiStore ep{c, ldc, 0, bias, bias_mod > 0 ? bias_mod : 1, 0, nullptr, 0, M, N, amax_c};
+    return launch_gemm_x3<RowK<LdDenseA>::template T, StagePre, EpiStore, true>(
+        MkRowK<LdDenseA>{LdDenseA{a, lda, M, K}, amax_a}, MkPre{reinterpret_cast<const __bf16*>(wx), N, amax_w}, ep, M,
+        N, K, 1, nterm, S(stream));
+}
 
 // slab[z][co][tap*Cin+ci] = partial sum over a pixel range of dY[pix][co] * X[pix+tap][ci]
 CDM_API int cdm_conv3x3_wgrad(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin,

@@ -108,8 +108,11 @@ class UNetEngine:
     """Kernel-level ContextUnet for one (n_feat, n_cfeat, height) on one device."""
 
     def __init__(self, n_feat: int, n_cfeat: int, height: int, device, conv_math: str = "fp32"):
-        if n_feat % 8 or height % 16:
-            raise ValueError("HIP path needs n_feat % 8 == 0 and height % 16 == 0")
+        # the reference needs height % 4 == 0 (two MaxPool2d(2), AvgPool2d(h/4), ConvTranspose2d(k = h/4):
+        # ContextUnet.py:17,27); the LDS-halo / band / fused paths take the map widths they support and every other
+        # width runs the generic kernels (round 5: heights 20, 36, 48 tested)
+        if n_feat % 8 or height % 4 or height < 4:
+            raise ValueError("HIP path needs n_feat % 8 == 0 and height % 4 == 0")
         if conv_math not in CONV_MATH:
             raise ValueError(f"conv_math must be one of {sorted(CONV_MATH)}")
         self.nf, self.ncf, self.H = n_feat, n_cfeat, height
@@ -153,6 +156,8 @@ class UNetEngine:
         # train: out.1's GroupNorm + ReLU inside out.3's forward and weight-gradient staging, zO never written
         # ($CDM_FUSE_GN_OUT=0: the apply kernel writes zO)
         self.fuse_gn_out = os.environ.get("CDM_FUSE_GN_OUT", "1") != "0"
+        # eval: the pool / FiLM / residual applies in the conv epilogue (fuses_eval)
+        self.fuse_eval = self.x16 and os.environ.get("CDM_FUSE_EVAL", "1") != "0"
         self.device = torch.device(device)
         self.layers = conv_layers(n_feat, height)
         self.L = {l.name: l for l in self.layers}
@@ -181,8 +186,9 @@ class UNetEngine:
     # weight packing (OIHW / [Cin][Cout][kh][kw] -> GEMM layouts; eval: BatchNorm folded)
     # ------------------------------------------------------------------------------------------
     def _repack_h3_train_batched(self, P, stream: int):
-        """h3 train mode: every 3x3 conv with C_in > 1 (and out.0) repacked in 3 launches — clear the max|W| slots,
-        max|W| per layer, the split images straight from OIHW (cdm_pack_split_conv3x3_batch)."""
+        """h3 / bf16 train mode: every 3x3 conv with C_in > 1 (and out.0) repacked in 3 launches — clear the max|W|
+        slots, max|W| per layer, the split images straight from OIHW (cdm_pack_split_conv3x3_batch; bf16: the one-term
+        hi plane, round 5 — it replaced 40 split + 18 pack launches per C4 step)."""
         nf = self.nf
         specs = [(l.name, P[l.w], l.cin, l.cout, l.kc) for l in self.layers if l.cin > 1]
         specs.append(("out.0", P["out.0.weight"], 2 * nf, nf, self.kc_out0))
@@ -202,7 +208,8 @@ class UNetEngine:
                 wdx = self._buf(name + ".wdg_x", (_cdiv(9 * cout, 16) * 3 * cin * 16,), torch.bfloat16)
                 self.pk[name + ".wpk_x"], self.pk[name + ".wdg_x"] = wx, wdx
                 self.pk[name + ".wpk_amax"] = self.pk[name + ".wdg_amax"] = slots[i:i + 1]
-                arr[i] = Job(W.data_ptr(), cin, cout, kc, 0, wx.data_ptr(), wdx.data_ptr(), slots.data_ptr() + 4 * i)
+                arr[i] = Job(W.data_ptr(), cin, cout, kc, 0 if self.h3 else 1, wx.data_ptr(), wdx.data_ptr(),
+                             slots.data_ptr() + 4 * i)
             raw = bytes(memoryview(arr).cast("B"))
             self._batch_jobs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
             self._batch_slots, self._batch_n = slots, len(specs)
@@ -217,7 +224,7 @@ class UNetEngine:
             return
         self.train_pack_token = None          # the pack changes owner (model.py re-packs before a stale backward)
         lb = lib(); nf = self.nf
-        batched = train and self.nterm == NT_H3 and self.batch_repack
+        batched = train and self.x16 and self.batch_repack
         if batched:
             self._repack_h3_train_batched(P, stream)
         for l in self.layers:
@@ -272,6 +279,8 @@ class UNetEngine:
             w0T = self._buf("up0.wtT", (self.KK0 * c0, c0))
             lb.cdm_pack_convT(_p(P["up0.0.weight"]), c0, c0, self.KK0, _p(w0), _p(w0T) if train else None, stream)
             self.pk["up0.wt"], self.pk["up0.wtT"] = w0, w0T
+            if self.x16:    # the forward GEMM on the 16-bit matrix cores (cdm_gemm_x16)
+                self._split("up0.wt", c0, self.KK0 * c0, stream)
         for m in MLPS:
             w2 = P[m + ".model.2.weight"]
             E = w2.shape[0]
@@ -485,6 +494,14 @@ class UNetEngine:
         c0 = 2 * nf
         if self.up0_large:
             lb.cdm_up0_fwd(_p(ws.hv), B, c0, _p(P["up0.0.weight"]), self.KK0, _p(P["up0.0.bias"]), _p(ws.y0), s)
+        elif self.x16:
+            # round 5: h3 / bf16 on the matrix cores (the fp32 MFMA GEMM took 105 us per sampling step at B = 256)
+            am_hv = None
+            if self.h3:
+                am_hv = _p(self._amax)
+                lb.cdm_amax_f32(_p(ws.hv), B, c0, c0, am_hv, 0, s)
+            lb.cdm_gemm_x16(_p(ws.hv), c0, B, c0, _p(self.pk["up0.wt_x"]), am_hv, self._wamax("up0.wt"),
+                            self.KK0 * c0, _p(ws.y0), self.KK0 * c0, _p(P["up0.0.bias"]), c0, None, self.nterm, s)
         else:
             lb.cdm_gemm_f32(_p(ws.hv), c0, B, c0, _p(self.pk["up0.wt"]), self.KK0 * c0, self.KK0 * c0, _p(ws.y0),
                             self.KK0 * c0, _p(P["up0.0.bias"]), c0, 0, 1, None, s)
@@ -581,6 +598,10 @@ class UNetEngine:
             if l.cin == 1:
                 lb.cdm_conv3x3_cin1_fwd(_p(x), B, S, S, _p(self.pk[l.name + ".wpk_e"]),
                                         _p(self.pk[l.name + ".bpk_e"]), outp.p, outp.ld, l.cout, 1, dslot, s)
+            elif not dense and self.fuses_eval(l, B):
+                # the residual add / FiLM / MaxPool in the conv's epilogue: y is never written
+                self._conv_eval_fused(ws, l, kind, x, s)
+                return
             else:
                 self.conv3x3(l.name + ".wpk_e", src.p, B, S, l.cin, src.ld, _p(self.pk[l.name + ".bpk_e"]), outp.p,
                              outp.ld, l.cout, EPI_RELU, None, 0, l.kc, s, amax_x=self._src_slot(ws, l),
@@ -610,6 +631,40 @@ class UNetEngine:
                                   0, _p(x), _p(sc_w), _p(sc_b), split, dst.p, dst.ld, am, s)
         else:
             raise AssertionError(kind)
+
+    def fuses_eval(self, l: "LayerSpec", B: int) -> bool:
+        """Eval forward of a pool / FiLM / residual layer with its output transform in the LDS-halo conv's epilogue
+        (cdm_conv3x3_fwd_x16_fused: 32^2 / 64^2 maps, 16-bit arithmetics); $CDM_FUSE_EVAL=0 keeps the apply kernel."""
+        return (self.fuse_eval and l.cin > 1 and l.kc == 16 and l.S in (32, 64) and l.cout % 128 == 0
+                and self.halo_addressable(B, l.S))
+
+    def _conv_eval_fused(self, ws, l: "LayerSpec", kind: str, x, s):
+        lb = lib()
+        B, S, C = ws.B, l.S, l.cout
+        src = ws.src[l.name]
+        dst = ws.dst[l.name]
+        key = l.name + ".wpk_e"
+        amax_x = self._src_slot(ws, l)
+        if self.h3 and amax_x is None:
+            amax_x = _p(self._amax)
+            lb.cdm_amax_f32(src.p, B * S * S, l.cin, src.ld, amax_x, 0, s)
+        sc_x = sc_w = sc_b = fa = fb = None
+        split = fan = fbn = 0
+        if kind == "resid":
+            code = 1
+            sc_w_t, sc_b_t, split = ws.sc_pending
+            sc_x, sc_w, sc_b = _p(x), _p(sc_w_t), _p(sc_b_t)
+        elif kind == "film":
+            code = 2
+            fa, fb = _p(ws.emb["contextembed2"]), _p(ws.emb["timeembed2"])
+            fan, fbn = (C if ws.c_rows > 1 else 0), (C if ws.t_rows > 1 else 0)
+        else:
+            assert kind == "pool", kind
+            code = 3
+        lb.cdm_conv3x3_fwd_x16_fused(src.p, B, S, S, l.cin, src.ld, _p(self.pk[key + "_x"]), amax_x,
+                                     self._wamax(key), _p(self.pk[l.name + ".bpk_e"]), dst.p, dst.ld, C, l.kc,
+                                     self._dst_slot(ws, l), code, sc_x, sc_w, sc_b, split, fa, fan, fb, fbn,
+                                     self.nterm, s)
 
     def _gn_fwd(self, ws, P, name, y: Act, B, S, C, st, stats_from_conv, stream):
         lb = lib()
@@ -947,7 +1002,10 @@ class UNetEngine:
                                         self.nterm, dt, s)
             lb.cdm_slab_reduce(_p(ws.slab), sp, cout, 9 * cin, _p(gW), 9 * cin, 1, 9, cin, 0, 1.0, s)
             return
-        if self.x16:
+        if S % 8:
+            # the 16-bit weight-gradient GEMMs stage 8-pixel pieces of one image row: other widths take the fp32 GEMM
+            lb.cdm_conv3x3_wgrad(dy.p, dy.ld, cout, x.p, B, S, S, cin, x.ld, sp, _p(ws.slab), s)
+        elif self.x16:
             am = _p(self._amax)
             if self.h3 and amax_dy is None:
                 amax_dy = am
@@ -973,17 +1031,18 @@ class UNetEngine:
         lb.cdm_slab_sum_all(_p(ws.dpart), nparts, 1, 0, 1, cout, _p(G[name + ".bias"]), 0, 1, 0, s)
         sp = wgrad_splits(B * Hin * Hin, cin, 4 * cout)
         x16 = self.x16
-        if x16:
+        if x16 and Hin % 8 == 0:
             prod = next(k for k, v in self._CONVT_GRAD_PRODUCERS.items() if v == name)
             a_gy = self._slot(ws, "gT:" + prod)
             a_x = self._slot(ws, {"up1.model.0": "catU1", "up2.model.0": "catU2"}[name])
             lb.cdm_convT2x2_wgrad_x16(x.p, B, Hin, Hin, cin, x.ld, gy.p, cout, gy.ld, a_x, a_gy, sp, _p(ws.slab),
                                       self.nterm, s)
-        else:
+        else:   # fp32 arithmetic, or an input grid whose width is not a multiple of 8 (the 16-bit GEMM's pieces)
             lb.cdm_convT2x2_wgrad(x.p, B, Hin, Hin, cin, x.ld, gy.p, cout, gy.ld, sp, _p(ws.slab), s)
         # slab[z][ci][ij*cout+co] -> [ci][co][ij]
         lb.cdm_slab_reduce(_p(ws.slab), sp, cin, 4 * cout, _p(G[name + ".weight"]), 4 * cout, 1, 4, cout, 0, 1.0, s)
-        if x16:
+        if self.x16:
+            a_gy = self._slot(ws, "gT:" + next(k for k, v in self._CONVT_GRAD_PRODUCERS.items() if v == name))
             lb.cdm_convT2x2_dgrad_x16(gy.p, B, Hin, Hin, cout, gy.ld, _p(self.pk[name + ".wtT_x"]), a_gy,
                                       self._wamax(name + ".wtT"), dx.p, dx.ld, cin, 0, self.nterm, s)
         else:

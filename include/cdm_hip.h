@@ -62,6 +62,16 @@ int cdm_conv3x3_fwd_h3_ex(const float* x, int N, int H, int W, int Cin, int ldx,
                           const void* wx, const float* amax_x, const float* amax_w, const float* bias, float* y, int ldy,
                           int Cout, int flags, float* stats, int stats_ld, int kc, float* amax_y, int* ymm, int ymm_ld,
                           void* stream);
+/* eval-mode conv3x3 of a Conv -> BatchNorm (folded into wx / bias) -> ReLU layer with its output transform in the
+ * LDS-halo epilogue (csrc/conv_fwd_eval.hip; W == H in {32, 64}, kc = 16, Cout % 128 == 0), v = relu(conv + bias):
+ *   kind 1 (resid, diffusion_utilities.py:54-55): y[p][c] = sc_w[s][c] sc_x[p] + sc_b[s][c] + v, s = image >= split
+ *   kind 2 (FiLM, ContextUnet.py:57-58):           y[p][c] = fa[image * fan + c] v + fb[image * fbn + c]
+ *   kind 3 (MaxPool2d(2), diffusion_utilities.py:109): y = the [N][H/2][W/2] pooled map (row stride ldy)
+ * amax_y (h3): running max|y|.  Replaces cdm_conv3x3_fwd_x16 + cdm_norm_apply_fwd of the eval forward. */
+int cdm_conv3x3_fwd_x16_fused(const float* x, int N, int H, int W, int Cin, int ldx, const void* wx,
+                              const float* amax_x, const float* amax_w, const float* bias, float* y, int ldy, int Cout,
+                              int kc, float* amax_y, int kind, const float* sc_x, const float* sc_w, const float* sc_b,
+                              int split, const float* fa, int fan, const float* fb, int fbn, int nterm, void* stream);
 /* timing ablations of the h3 LDS-halo conv (64x64 maps, no bias / stats; tools/conv_ablation.py): abl bits
  * 1 fragment prefetch, 2 MFMAs doubled, 4 B staged once, 8 halo without the term split (results meaningless);
  * bits 16+: tiles per block (0 -> 1) */
@@ -209,6 +219,12 @@ int cdm_convT2x2_dgrad(const float* dy, int N, int H, int W, int Cout, int lddy,
 int cdm_gemm_f32(const float* a, long long lda, int M, int K, const float* b, long long ldb, int N, float* c,
                  long long ldc, const float* bias, int bias_mod, int flags, int splits, float* slab, void* stream);
 int cdm_gemm_splits(int K, int splits);
+/* C[m][n] = A[m][k] . B[k][n] + bias[n % bias_mod] on the 16-bit matrix cores (nterm 4 = h3, 1 = bf16); wx = the split
+ * image of B [K][N] (cdm_split_f16x2 with max|B| in *amax_w / cdm_split_bf16x3); h3: max|A| = *amax_a; amax_c
+ * (optional): running max|C|.  The up0 ConvTranspose2d(k = h/4) of the 1x1 map (ContextUnet.py:26-30). */
+int cdm_gemm_x16(const float* a, long long lda, int M, int K, const void* wx, const float* amax_a, const float* amax_w,
+                 int N, float* c, long long ldc, const float* bias, int bias_mod, float* amax_c, int nterm,
+                 void* stream);
 /* weight gradients (autograd of the layers above), split-K partial slabs [splits][M][N]. */
 int cdm_conv3x3_wgrad(const float* dy, int lddy, int Cout, const float* x, int N, int H, int W, int Cin, int ldx,
                       int splits, float* slab, void* stream);

@@ -193,21 +193,16 @@ def test_unet_down_up_backward():
     _grad_check(up, gu, ref_up, gu, [torch.randn(2, 32, 8, 8), torch.randn(2, 32, 8, 8)])
 
 
-@pytest.mark.parametrize("in_dim", [6, 8])
+@pytest.mark.parametrize("in_dim", [1, 5, 6, 8])
 def test_embed_fc_backward(in_dim):
+    """EmbedFC alone, parameter and input gradients for every input_dim (the reference's t embedding takes 1, its
+    context embeddings n_cfeat = 5 or 6: diffusion_utilities.py:118-145, ContextUnet.py:22-23)."""
     from cdm_amd import EmbedFC
     torch.manual_seed(14)
     cpu = EmbedFC(in_dim, 64)
     gpu = copy.deepcopy(cpu).cuda()
     x = torch.rand(5, in_dim)
-    if in_dim % 4 == 0:
-        _grad_check(cpu, gpu, lambda v: cpu.model(v.view(-1, in_dim)), gpu, [x])
-    else:   # parameter gradients (the time / context inputs of ContextUnet need none)
-        g = torch.randn(5, 64)
-        (cpu.model(x) * g).sum().backward()
-        (gpu(x.cuda()) * g.cuda()).sum().backward()
-        for (n, p), r in zip(gpu.named_parameters(), cpu.parameters()):
-            assert ((p.grad.cpu() - r.grad).norm() / r.grad.norm()).item() < 1e-5, n
+    _grad_check(cpu, gpu, lambda v: cpu.model(v.view(-1, in_dim)), gpu, [x])
 
 
 @pytest.mark.parametrize("kind", ["rcb", "down", "cin1_res"])

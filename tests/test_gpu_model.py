@@ -373,3 +373,96 @@ def test_eval_pack_not_shared_across_models():
         assert _rel(eps, ref) < 2e-4, seed
         del m, eps
         gc.collect()
+
+
+@pytest.mark.parametrize("math", ["h3", "bf16"])
+def test_eval_fused_epilogue_matches_apply_kernel(math):
+    """The eval forward's residual / FiLM / MaxPool applies in the conv epilogue (cdm_conv3x3_fwd_x16_fused,
+    engine.fuses_eval) vs the conv + cdm_norm_apply_fwd pair they replace, n_feat = 128 (the fused shapes: 64^2 residual
+    and pool, 32^2 FiLM and pool), per-sample t / c and a broadcast t: the same values (bit-identical or within
+    1e-6 of max|eps|; recorded), and a CFG sampling run (two shortcut sets, the batched 2n forward) likewise."""
+    import cdm_amd
+    from cdm_amd.diffusion import GraphSampler, Schedule
+    m = _model(128, math=math).eval()
+    eng, _ = m._engine_and_params()
+    assert eng.fuse_eval
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(3, 1, 64, 64, generator=g).cuda()
+    c = torch.rand(3, 6, generator=g).cuda()
+    res = {}
+    for tb in (torch.rand(3, generator=g).cuda(), torch.rand(1, generator=g).cuda()):
+        outs = []
+        for fuse in (True, False):
+            eng.fuse_eval = fuse
+            torch.manual_seed(7)
+            with torch.no_grad():
+                outs.append(m(x, tb, c).cpu())
+        d = (outs[0] - outs[1]).abs().max().item() / outs[1].abs().max().item()
+        res[f"t_rows_{tb.numel()}"] = d
+        assert d <= 1e-6, d
+    params = torch.rand(2, 6, generator=torch.Generator().manual_seed(3))
+    sched = Schedule(12, "cuda")
+    xs = []
+    for fuse in (True, False):
+        eng.fuse_eval = fuse
+        smp = GraphSampler(m, sched, 2, 3.0, params, z_source="device", seed=5, use_graph=False)
+        torch.manual_seed(4)
+        smp.prepare_rng(host_z=False)
+        xT = torch.randn(2, 1, 64, 64, generator=torch.Generator().manual_seed(2))
+        xs.append(smp.run(xT)[0].cpu())
+    eng.fuse_eval = True
+    d = (xs[0] - xs[1]).abs().max().item() / xs[1].abs().max().item()
+    res["cfg_sample"] = d
+    print(math, "fused vs apply kernel, max rel diff:", res)
+    assert d <= 1e-5, d
+
+
+@pytest.mark.parametrize("H", [20, 36, 48])
+def test_map_heights_not_multiple_of_16(H):
+    """ContextUnet(height=H) for any H % 4 == 0 (the reference's only requirement: ContextUnet.py:17,27 — two MaxPool2d(2),
+    AvgPool2d(H/4), ConvTranspose2d(k = H/4)); widths outside the LDS-halo / band kernels' set run the generic kernels
+    (split GEMM convs, fp32 weight-gradient GEMMs for widths % 8 != 0).  n_feat 16, B 2, h3: forward train / eval vs
+    the fp32 oracle (2e-4) and every parameter gradient vs fp64 (the test_train_grads_random_weights_vs_fp64 bar)."""
+    from cdm_amd import ContextUnet
+    nf, B, T = 16, 2, 1500
+    torch.manual_seed(23)
+    m = ContextUnet(1, nf, 6, H).cuda()
+    sd = R.clone_sd(m.state_dict())
+    g = torch.Generator().manual_seed(31)
+    x = torch.rand(B, 1, H, H, generator=g); noise = torch.randn(B, 1, H, H, generator=g)
+    c = torch.rand(B, 6, generator=g); tt = torch.randint(1, T + 1, (B,), generator=g)
+    for train in (False, True):
+        m.train(train)
+        with torch.no_grad():
+            torch.manual_seed(21)
+            eps = m(x.cuda(), (tt / T).cuda(), c.cuda())
+        torch.manual_seed(21)
+        ref = R.unet_forward(R.clone_sd(sd), x, tt / T, c, n_feat=nf, n_cfeat=6, height=H, train=train,
+                             shortcut=lambda: R.draw_shortcut(1, nf))
+        assert _rel(eps, ref) < 2e-4, (H, train, _rel(eps, ref))
+    m.load_state_dict(sd)
+    m.train()
+    _, _, ab = R.make_schedule(T)
+    xp = R.perturb_input(x, tt, noise, ab)
+    torch.manual_seed(33)
+    pred = m(xp.cuda(), (tt / T).cuda(), c.cuda())
+    F.mse_loss(pred, noise.cuda()).backward()
+
+    def oracle(dtype):
+        s = {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+        tr = R.OracleTrainer(s, n_feat=nf, n_cfeat=6, height=H)
+        torch.manual_seed(33)
+        w, b = R.draw_shortcut(1, nf)
+        return tr.step(x.to(dtype), c.to(dtype), noise.to(dtype), tt, T, ab.to(dtype), (w.to(dtype), b.to(dtype)))
+    _, p64, g64 = oracle(torch.float64)
+    assert _rel(pred.double(), p64) < 2e-4
+    gmax = max(v.abs().max().item() for v in g64.values())
+    errs = {}
+    for k, p in m.named_parameters():
+        got = p.grad.cpu().double()
+        if ".conv1.0.bias" in k or ".conv2.0.bias" in k:
+            assert got.abs().max().item() <= 1e-4 * gmax, k
+        else:
+            errs[k] = ((got - g64[k]).norm() / g64[k].norm()).item()
+    print(f"H={H}: grads vs fp64 max {max(errs.values()):.2e} median {np.median(list(errs.values())):.2e}")
+    assert max(errs.values()) <= 1e-2 and float(np.median(list(errs.values()))) <= 5e-3
