@@ -525,7 +525,8 @@ class UNetEngine:
         self.conv3x3("out.0.wpk", ws.catO.p, B, H, 2 * nf, 2 * nf, _p(P["out.0.bias"]), _p(ws.yO), nf, nf, 0,
                      _p(ws.slab), nf, self.kc_out0, s, amax_x=self._slot(ws, "catO"))
         probe("yO", ws)
-        self._gn_fwd(ws, P, "out.1", Act(ws.yO, nf), B, H, nf, ws.gnO, stats_from_conv=True, stream=s)
+        # out.1's GroupNorm statistics come from out.0's epilogue partials (128-pixel tiles) when no tile spans two images
+        self._gn_fwd(ws, P, "out.1", Act(ws.yO, nf), B, H, nf, ws.gnO, stats_from_conv=(H * H) % CHUNK == 0, stream=s)
         if self.fuses_gn_out(train):
             # out.1's GroupNorm + ReLU applied in out.3's staging (train: and in out.3's weight gradient): zO never
             # written

@@ -4,7 +4,8 @@ code/diffusion_utilities.py:137-145 views to [-1, in_dim]), against torch autogr
 
 Tolerance (_branch_check): relative L2 of each input gradient and of every parameter gradient vs an fp64 autograd run
 of the oracle on the same branch of the piecewise-linear network (HIP's own ReLU / MaxPool decisions imposed), at most 3x
-the reference's own fp32 deviation from fp64 on ITS branch plus a floor of 2e-6 (the fp32 rounding of a gradient the
+the reference's own fp32 deviation from fp64 on ITS branch (the larger of two of its runs whose CPU reductions add in
+different orders) plus a floor of 2e-6 (the fp32 rounding of a gradient the
 network barely amplifies).  Train-mode BatchNorm, n_feat = 16, B = 4, input seeds 0..2 (round 4 selected a seed on which
 no arithmetic flips a decision; round 5's audit, tools/kink_diag.py / profiles/r5_kink_diag.txt, found HIP's per-layer
 pre-activation errors equal to or below the reference's on every layer — the flips are single elements at |z| below
@@ -16,6 +17,7 @@ import torch
 
 from oracle import ref_cpu as R
 import _parity
+from _kinks import Kinks, hip_kinks
 
 pytestmark = pytest.mark.gpu
 
@@ -32,52 +34,6 @@ NF, NCF, H, B = 16, 6, 64, 4
 def _rel_l2(a, b):
     a = torch.as_tensor(a).double().cpu(); b = torch.as_tensor(b).double().cpu()
     return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
-
-
-class _Kinks:
-    """The oracle's ReLU / MaxPool decisions (torch.nn.functional calls of oracle/ref_cpu.py's forward, in call order):
-    capture=True records them (relu: mask z > 0 and z; max_pool2d(2): the first-max index of each 2x2 window, the
-    order of torch's CPU kernel); otherwise the given decisions are imposed — relu(z) = z * mask, the pool output taken
-    at the given index — so autograd runs the backward of THAT branch of the piecewise-linear network."""
-
-    def __init__(self, relu=None, pool=None):
-        self.capture = relu is None
-        self.relu, self.pool = ([], []) if self.capture else (list(relu), list(pool))
-
-    def __enter__(self):
-        self._relu, self._pool = R.F.relu, R.F.max_pool2d
-        it_r, it_p = iter(self.relu), iter(self.pool)
-
-        def relu(z, inplace=False):
-            if self.capture:
-                self.relu.append(((z > 0).detach().clone(), z.detach().clone()))
-                return self._relu(z)
-            return z * next(it_r)[0].to(z.dtype)
-
-        def pool(v, k, *a, **kw):
-            B, C, H, W = v.shape
-            win = v.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
-            if self.capture:
-                self.pool.append(_first_max(win.detach()))
-                return self._pool(v, k, *a, **kw)
-            return win.gather(-1, next(it_p).unsqueeze(-1)).squeeze(-1)
-        R.F.relu, R.F.max_pool2d = relu, pool
-        return self
-
-    def __exit__(self, *exc):
-        R.F.relu, R.F.max_pool2d = self._relu, self._pool
-
-
-def _first_max(win):
-    """index of the first maximum over the last axis (NaN wins, as torch's CPU max_pool2d and the HIP pool apply)"""
-    best = win[..., 0].clone()
-    arg = torch.zeros(best.shape, dtype=torch.int64)
-    for e in range(1, win.shape[-1]):
-        v = win[..., e]
-        take = (v > best) | torch.isnan(v)
-        best = torch.where(take, v, best)
-        arg = torch.where(take, torch.full_like(arg, e), arg)
-    return arg
 
 
 def _oracle(sd, x, t, c, sc, dtype, weight, train=True, kinks=None):
@@ -98,61 +54,37 @@ def _oracle(sd, x, t, c, sc, dtype, weight, train=True, kinks=None):
     return eps.detach(), xx.grad, tt.grad, cc.grad, {k: sd[k].grad for k in keys}
 
 
-def _hip_kinks(m, x, t, c, sc, frozen):
-    """HIP's decisions in the oracle's call order, from one engine forward on the same inputs (deterministic, the
-    kernels of the module call): per ReLU the mask of z = fma(y, s, t) > 0 (NCHW) and z, per MaxPool the first-max index
-    of relu(z) over each window (the pool apply's order).  Call order: the 10 encoder Conv-BN-ReLU layers (a pool after
-    the 6th and the 10th), up0's GroupNorm-ReLU, the 8 decoder layers, out.1's GroupNorm-ReLU."""
-    eng, P = m._engine_and_params()
-    s = torch.cuda.current_stream().cuda_stream
-    eng.repack(P, True, s)
-    ws = eng.workspace(B, True, frozen=frozen)
-    eng.forward(ws, P, x.cuda().reshape(B, H, H), t.cuda(), c.cuda(), sc[0].reshape(-1).cuda(), sc[1].cuda(), B, s,
-                frozen=frozen)
-    torch.cuda.synchronize()
-
-    def z_of(y, scale, shift, C, S, per_sample):
-        y = y.double().cpu().reshape(B, S, S, C)
-        sc_ = scale.double().cpu().reshape(B if per_sample else 1, 1, 1, C)
-        sh = shift.double().cpu().reshape(B if per_sample else 1, 1, 1, C)
-        z = (y * sc_ + sh).float().permute(0, 3, 1, 2).contiguous()
-        return z
-
-    relu, pool = [], []
-    L = eng.layers
-    for i, l in enumerate(L):
-        st = ws.bn[l.name]
-        z = z_of(ws.y[l.name], st["scale"], st["shift"], l.cout, l.S, False)
-        relu.append((z > 0, z))
-        if l.name in ("down1.model.1.conv2", "down2.model.1.conv2"):
-            Bz, C, S, _ = z.shape
-            r = torch.relu(z)
-            win = r.reshape(Bz, C, S // 2, 2, S // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(Bz, C, S // 2, S // 2, 4)
-            pool.append(_first_max(win))
-        if i == 9:
-            z0 = z_of(ws.y0, ws.gn0["scale"], ws.gn0["shift"], 2 * NF, H // 4, True)
-            relu.append((z0 > 0, z0))
-    zO = z_of(ws.yO, ws.gnO["scale"], ws.gnO["shift"], NF, H, True)
-    relu.append((zO > 0, zO))
-    return relu, pool
-
-
 def _branch_check(tag, m, sd, inputs, hip_grads, train, rec):
     """HIP's gradients vs fp64 autograd of the oracle on HIP's own branch (its ReLU / MaxPool decisions imposed) and the
-    reference's fp32 gradients vs fp64 on the reference's branch: a ReLU / MaxPool decision at |z| of the rounding error
+    reference's fp32 gradients vs fp64 on the reference's branch (the larger error of its runs on this host's threads and
+    on one thread, per tensor): a ReLU / MaxPool decision at |z| of the rounding error
     is a discrete choice either arithmetic may make (both are exact gradients of their branch); the bar compares the
     arithmetic error of each on its own branch — every tensor within 3x the reference's + 2e-6.  Also held: HIP's
     per-layer pre-activation error within 3x the reference's, and the decisions each arithmetic flips relative to fp64
     are counted (recorded)."""
     x, t, c, sc, weight = inputs
-    cap64, cap32 = _Kinks(), _Kinks()
+    cap64 = Kinks()
     _oracle(sd, x, t, c, sc, torch.float64, weight, train, cap64)
-    e32, dx32, dt32, dc32, g32 = _oracle(sd, x, t, c, sc, torch.float32, weight, train, cap32)
-    hk_relu, hk_pool = _hip_kinks(m, x, t, c, sc, frozen=not train)
+    hk_relu, hk_pool = hip_kinks(m, x, t, c, sc, frozen=not train)
     assert len(hk_relu) == len(cap64.relu) == 20 and len(hk_pool) == len(cap64.pool) == 2
-    e64h, dx64h, dt64h, dc64h, g64h = _oracle(sd, x, t, c, sc, torch.float64, weight, train, _Kinks(hk_relu, hk_pool))
-    e64r, dx64r, dt64r, dc64r, g64r = _oracle(sd, x, t, c, sc, torch.float64, weight, train,
-                                              _Kinks(cap32.relu, cap32.pool))
+    e64h, dx64h, dt64h, dc64h, g64h = _oracle(sd, x, t, c, sc, torch.float64, weight, train, Kinks(hk_relu, hk_pool))
+    # the reference's own fp32 error: its run on this host's threads and its run on one thread (torch's CPU reductions
+    # — batch-norm sums, weight-gradient sums over pixels — add in another order), each vs fp64 on its own branch; the
+    # per-tensor larger of the two is the envelope HIP is held to (one fp32 run's error on a cancelling reduction, e.g.
+    # a BatchNorm weight gradient, is one draw that may land far below its typical size)
+    refs = []
+    nthreads = torch.get_num_threads()
+    try:
+        for th in (nthreads, 1):
+            torch.set_num_threads(th)
+            cap32 = Kinks()
+            r32 = _oracle(sd, x, t, c, sc, torch.float32, weight, train, cap32)
+            r64 = _oracle(sd, x, t, c, sc, torch.float64, weight, train, Kinks(cap32.relu, cap32.pool))
+            refs.append((cap32, r32, r64))
+    finally:
+        torch.set_num_threads(nthreads)
+    cap32, (e32, dx32, dt32, dc32, g32), (e64r, dx64r, dt64r, dc64r, g64r) = refs[0]
+    (_, r32b, r64b) = refs[1]
     flips_h = sum(int((a[0] != b[0]).sum()) for a, b in zip(hk_relu, cap64.relu)) + \
         sum(int((a != b).sum()) for a, b in zip(hk_pool, cap64.pool))
     flips_r = sum(int((a[0] != b[0]).sum()) for a, b in zip(cap32.relu, cap64.relu)) + \
@@ -166,16 +98,18 @@ def _branch_check(tag, m, sd, inputs, hip_grads, train, rec):
             zbad.append((j, eh, er))
     hip_eps, hip_dx, hip_dt, hip_dc, hip_p = hip_grads
     bad = []
-    if _rel_l2(hip_eps, e64h) > 3 * _rel_l2(e32, e64r) + 2e-6:
-        bad.append(("eps", _rel_l2(hip_eps, e64h), _rel_l2(e32, e64r)))
-    items = [("x", hip_dx, dx64h, dx32, dx64r), ("t", hip_dt, dt64h, dt32, dt64r), ("c", hip_dc, dc64h, dc32, dc64r)]
-    items += [(k, hip_p[k], g64h[k], g32[k], g64r[k]) for k in g64h]
+    e_ref = max(_rel_l2(e32, e64r), _rel_l2(r32b[0], r64b[0]))
+    if _rel_l2(hip_eps, e64h) > 3 * e_ref + 2e-6:
+        bad.append(("eps", _rel_l2(hip_eps, e64h), e_ref))
+    items = [("x", hip_dx, dx64h, (dx32, dx64r), (r32b[1], r64b[1])), ("t", hip_dt, dt64h, (dt32, dt64r), (r32b[2], r64b[2])),
+             ("c", hip_dc, dc64h, (dc32, dc64r), (r32b[3], r64b[3]))]
+    items += [(k, hip_p[k], g64h[k], (g32[k], g64r[k]), (r32b[4][k], r64b[4][k])) for k in g64h]
     worst = 0.0
-    for name, hip, r64h, r32, r64r in items:
+    for name, hip, r64h, (r32, r64r), (r32_1, r64_1) in items:
         assert hip is not None and tuple(hip.shape) == tuple(r64h.shape), name
         if r64h.norm() == 0 and r64r.norm() == 0:
             continue
-        eh, er = _rel_l2(hip, r64h), _rel_l2(r32, r64r)
+        eh, er = _rel_l2(hip, r64h), max(_rel_l2(r32, r64r), _rel_l2(r32_1, r64_1))
         rec[name] = (eh, er)
         worst = max(worst, eh / (3 * er + 2e-6))
         if eh > 3 * er + 2e-6:

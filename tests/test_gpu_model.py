@@ -133,13 +133,17 @@ def test_forward_random_weights_vs_oracle(nf, B, math):
         assert _rel(eps, ref) < 2e-4, (train, _rel(eps, ref))
 
 
-def _oracle_grads(sd, x, c, noise, tt, T, ab, nf, dtype, seed):
+def _oracle_grads(sd, x, c, noise, tt, T, ab, nf, dtype, seed, kinks=None):
+    """the oracle train step (perturb + forward + mse + backward) -> (pred, grads); kinks: a _kinks.Kinks context
+    around it (capture the branch, or impose one)"""
+    import contextlib
     s = {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in sd.items()}
     tr = R.OracleTrainer(s, n_feat=nf, n_cfeat=6, height=64)
     torch.manual_seed(seed)
     w, b = R.draw_shortcut(1, nf)
-    _, pred, grads = tr.step(x.to(dtype), c.to(dtype), noise.to(dtype), tt, T, ab.to(dtype),
-                             (w.to(dtype), b.to(dtype)))
+    with (kinks if kinks is not None else contextlib.nullcontext()):
+        _, pred, grads = tr.step(x.to(dtype), c.to(dtype), noise.to(dtype), tt, T, ab.to(dtype),
+                                 (w.to(dtype), b.to(dtype)))
     return pred, grads
 
 
@@ -152,16 +156,20 @@ def test_train_grads_random_weights_vs_fp64(nf, math):
     """HIP grads vs an fp64 oracle, at the accuracy the reference's own fp32 CPU path has (n_feat 64 and the
     C2 width 128, where all 12 fused BN-backward layers run under h3).
 
-    Rationale: with ReLU + MaxPool, last-bit differences flip a handful of kink decisions (|z| ~ 1e-6)
-    and each flip propagates to every layer upstream of it.  For the nf=64 input the reference CPU
-    path in fp32 vs fp64 shows relative-L2 errors up to 3.8e-3 (a flip in down2), the HIP path up to
-    4.1e-3 (a flip in up2).  Criterion, relative L2 vs fp64: every tensor <= 1e-2, and the median
-    over tensors <= 5e-3.  Conv biases feeding a BatchNorm have an analytic gradient of 0 (rounding
-    noise only): |g| <= 1e-4 * max grad.  The strict check lives in test_train_step_grads_match_reference.
+    With ReLU + MaxPool, last-bit differences flip kink decisions at |z| ~ 1e-6 (either arithmetic may take either
+    side; each flip reroutes a gradient upstream — relative L2 1e-3 .. 1e-2 vs a run that did not flip).  Round 5
+    compares each arithmetic on its own branch (tests/_kinks.py): HIP vs fp64 autograd with HIP's decisions imposed,
+    the reference's fp32 run vs fp64 with its own decisions imposed — the larger of its runs on this host's threads and
+    on one thread (other CPU reduction orders).  Criterion per tensor: HIP <= 3x the reference + 2e-6; median over
+    tensors <= 3x the reference's median.  Conv biases feeding a BatchNorm have an analytic gradient of 0 (rounding
+    noise only): |g| <= 1e-4 * max grad.  The decisions each flips relative to plain fp64 are recorded.
     """
+    import _parity
+    from _kinks import Kinks, hip_kinks
     B, T = 2, 1500
     seed = {64: 4, 128: 14}[nf]
     m = _model(nf, seed=seed, math=math).train()
+    sd = R.clone_sd(_model(nf, seed=seed, math=math).state_dict())
     g = torch.Generator().manual_seed(10)
     x = torch.rand(B, 1, 64, 64, generator=g); noise = torch.randn(B, 1, 64, 64, generator=g)
     c = torch.rand(B, 6, generator=g); tt = torch.randint(1, T + 1, (B,), generator=g)
@@ -171,11 +179,29 @@ def test_train_grads_random_weights_vs_fp64(nf, math):
     pred = m(xp.cuda(), (tt / T).cuda(), c.cuda())
     F.mse_loss(pred, noise.cuda()).backward()
     if nf not in _ORACLE_CACHE:
-        sd = R.clone_sd(_model(nf, seed=seed, math=math).state_dict())
-        _ORACLE_CACHE[nf] = (_oracle_grads(sd, x, c, noise, tt, T, ab, nf, torch.float32, 33),
-                             _oracle_grads(sd, x, c, noise, tt, T, ab, nf, torch.float64, 33))
-    (p32, g32), (p64, g64) = _ORACLE_CACHE[nf]
+        refs = []
+        nthreads = torch.get_num_threads()
+        try:
+            for th in (nthreads, 1):
+                torch.set_num_threads(th)
+                cap = Kinks()
+                _, g32 = _oracle_grads(sd, x, c, noise, tt, T, ab, nf, torch.float32, 33, cap)
+                _, g64r = _oracle_grads(sd, x, c, noise, tt, T, ab, nf, torch.float64, 33, Kinks(cap.relu, cap.pool))
+                refs.append((g32, g64r))
+        finally:
+            torch.set_num_threads(nthreads)
+        cap64 = Kinks()
+        _oracle_grads(sd, x, c, noise, tt, T, ab, nf, torch.float64, 33, cap64)
+        _ORACLE_CACHE[nf] = (refs, cap64)
+    refs, cap64 = _ORACLE_CACHE[nf]
+    torch.manual_seed(33)
+    sc = R.draw_shortcut(1, nf)
+    m.load_state_dict(sd)
+    hk_relu, hk_pool = hip_kinks(m, xp, tt / T, c, sc, frozen=False)
+    p64, g64 = _oracle_grads(sd, x, c, noise, tt, T, ab, nf, torch.float64, 33, Kinks(hk_relu, hk_pool))
     assert _rel(pred.double(), p64) < 2e-4
+    flips = sum(int((a[0] != b[0]).sum()) for a, b in zip(hk_relu, cap64.relu)) + \
+        sum(int((a != b).sum()) for a, b in zip(hk_pool, cap64.pool))
     gmax = max(v.abs().max().item() for v in g64.values())
     bad, errs, errs32 = [], [], []
     for k, p in m.named_parameters():
@@ -183,19 +209,21 @@ def test_train_grads_random_weights_vs_fp64(nf, math):
         got = p.grad.cpu().double()
         if ".conv1.0.bias" in k or ".conv2.0.bias" in k:
             ok = got.abs().max().item() <= 1e-4 * gmax
-            print(f"{k:40s} |g| {got.abs().max().item():.2e} (analytic 0)")
         else:
             e_hip = ((got - ref).norm() / ref.norm()).item()
-            e_cpu = ((g32[k].double() - ref).norm() / ref.norm()).item()
-            ok = e_hip <= 1e-2
+            e_cpu = max(((g32[k].double() - g64r[k]).norm() / g64r[k].norm()).item() for g32, g64r in refs)
+            ok = e_hip <= 3 * e_cpu + 2e-6
             errs.append(e_hip); errs32.append(e_cpu)
             print(f"{k:40s} l2rel hip {e_hip:.2e} cpu32 {e_cpu:.2e}")
         if not ok:
             bad.append(k)
-    print(f"nf={nf} [{math}]: median rel L2 hip {np.median(errs):.2e} (reference fp32 {np.median(errs32):.2e}), "
-          f"max hip {max(errs):.2e} (reference fp32 {max(errs32):.2e})")
+    print(f"nf={nf} [{math}]: HIP flips {flips} decisions vs plain fp64; on each run's own branch: median rel L2 hip "
+          f"{np.median(errs):.2e} (reference fp32 {np.median(errs32):.2e}), max hip {max(errs):.2e} (reference fp32 "
+          f"{max(errs32):.2e})")
+    _parity.record("train_grads_branch", nf=nf, conv_math=math, flips_hip=flips, hip_median=float(np.median(errs)),
+                   ref32_median=float(np.median(errs32)), hip_max=max(errs), ref32_max=max(errs32))
     assert not bad, bad
-    assert float(np.median(errs)) <= 5e-3
+    assert float(np.median(errs)) <= 3 * float(np.median(errs32))
 
 
 def test_fused_bn_bwd_matches_unfused_nf128():
