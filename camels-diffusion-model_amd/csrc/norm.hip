@@ -21,7 +21,8 @@ struct NormP {              // z_pre = y*s + t ; xhat = (y - mean)*invstd
     const float* mean; const float* invstd; int mn; int cpg;  // index n*mn + c/cpg
 };
 struct FilmP { const float* a; int an; const float* b; int bn; };  // out = a[n*an+c]*u + b[n*bn+c]
-struct ResidP { const float* x; const float* w; const float* b; int split; };  // + w[c]*x[n,p] + b[c] (C_in = 1)
+// + w[c]*x[n,p] + b[c] (C_in = 1), or + b[c] + sum_k w[c][k] x[n,p][k] over xc image channels (x pixel stride ldx)
+struct ResidP { const float* x; const float* w; const float* b; int split; int xc = 1; int ldx = 1; };
 
 // -------------------------------------------------------------------------------------------------
 // generic per-(n,c) partial reduction over pixel chunks
@@ -469,7 +470,15 @@ __global__ __launch_bounds__(256) void norm_apply_fwd_kernel(const float* y, int
                 if constexpr (FILM) z = fp.a[n * fp.an + c] * z + fp.b[n * fp.bn + c];
                 if constexpr (RESID) {
                     const int sel = n >= rp.split ? C : 0;
-                    z = rp.w[sel + c] * rp.x[pix] + rp.b[sel + c] + z;
+                    if (rp.xc == 1) {
+                        z = rp.w[sel + c] * rp.x[pix] + rp.b[sel + c] + z;
+                    } else {   // in_channels > 1: the 1x1 shortcut's dot product over the image channels
+                        const float* wr = rp.w + (long long)(sel + c) * rp.xc;
+                        const float* xr = rp.x + pix * rp.ldx;
+                        float r = rp.b[sel + c];
+                        for (int k = 0; k < rp.xc; ++k) r = fmaf(wr[k], xr[k], r);
+                        z = r + z;
+                    }
                 }
                 o[j] = z;
             }
@@ -831,6 +840,26 @@ CDM_API int cdm_norm_apply_fwd(int flags, const float* y, int ldy, int N, int H,
         if (relu) CDM_APPLY(false, false, false, true); else CDM_APPLY(false, false, false, false);
     }
 #undef CDM_APPLY
+    return cdm_status();
+}
+
+// the residual apply of ResidualConvBlock(in_channels > 1, C, is_res) (diffusion_utilities.py:45-55 with the fresh 1x1
+// shortcut of :54): out = [relu](y s + t) + rb[c] + sum_k rw[c][k] rx[p][k], k < xc image channels at pixel stride ldx
+// (rw / rb: [2][C][xc] / [2][C] when rsplit < N, the CFG halves' two draws)
+CDM_API int cdm_norm_apply_fwd_resid_c(int relu, const float* y, int ldy, int N, int H, int W, int C, const float* s,
+                                       const float* t, const float* rx, int ldx, int xc, const float* rw, const float* rb,
+                                       int rsplit, float* out, int ldo, float* amax, void* stream) {
+    if (C % 4 || xc < 1 || ldx < xc) return (int)hipErrorInvalidValue;
+    NormP np{s, t, 0, nullptr, nullptr, 0, 1};
+    FilmP fp{nullptr, 0, nullptr, 0};
+    ResidP rp{rx, rw, rb, rsplit, xc, ldx};
+    const int nb = ew_blocks((long long)N * H * W * (C / 4));
+    if (relu)
+        hipLaunchKernelGGL((norm_apply_fwd_kernel<false, false, true, true>), dim3(nb), dim3(256), 0, S(stream), y, ldy, N,
+                           H, W, C, np, fp, rp, out, ldo, amax);
+    else
+        hipLaunchKernelGGL((norm_apply_fwd_kernel<false, false, true, false>), dim3(nb), dim3(256), 0, S(stream), y, ldy,
+                           N, H, W, C, np, fp, rp, out, ldo, amax);
     return cdm_status();
 }
 

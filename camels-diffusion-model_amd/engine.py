@@ -78,14 +78,16 @@ def conv_kc(cin: int, cout: int) -> int:
     return 16 if (cin % 16 == 0 and cout % 16 == 0) else 0
 
 
-def conv_layers(nf: int, H: int):
+def conv_layers(nf: int, H: int, cin0: int = 1):
+    """The 18 Conv3x3 -> BatchNorm -> ReLU layers in forward order; cin0 = the image channels the init conv reads
+    (in_channels, padded to a multiple of 4 when > 1)."""
     L = []
 
     def rcb(prefix, cin, cout, S):
         L.append(LayerSpec(prefix + ".conv1", cin, cout, S))
         L.append(LayerSpec(prefix + ".conv2", cout, cout, S))
 
-    rcb("init_conv", 1, nf, H)
+    rcb("init_conv", cin0, nf, H)
     rcb("down1.model.0", nf, nf, H); rcb("down1.model.1", nf, nf, H)
     rcb("down2.model.0", nf, 2 * nf, H // 2); rcb("down2.model.1", 2 * nf, 2 * nf, H // 2)
     rcb("up1.model.1", nf, nf, H // 2); rcb("up1.model.2", nf, nf, H // 2)
@@ -107,7 +109,7 @@ MLPS = ("contextembed1", "timeembed1", "contextembed2", "timeembed2")
 class UNetEngine:
     """Kernel-level ContextUnet for one (n_feat, n_cfeat, height) on one device."""
 
-    def __init__(self, n_feat: int, n_cfeat: int, height: int, device, conv_math: str = "fp32"):
+    def __init__(self, n_feat: int, n_cfeat: int, height: int, device, conv_math: str = "fp32", in_channels: int = 1):
         # the reference needs height % 4 == 0 (two MaxPool2d(2), AvgPool2d(h/4), ConvTranspose2d(k = h/4):
         # ContextUnet.py:17,27); the LDS-halo / band / fused paths take the map widths they support and every other
         # width runs the generic kernels (round 5: heights 20, 36, 48 tested)
@@ -116,6 +118,13 @@ class UNetEngine:
         if conv_math not in CONV_MATH:
             raise ValueError(f"conv_math must be one of {sorted(CONV_MATH)}")
         self.nf, self.ncf, self.H = n_feat, n_cfeat, height
+        # image channels (ContextUnet.py:6,14,39).  The reference's call sites all build in_channels = 1, for which the
+        # C_in = 1 init-conv kernels and the C_out = 1 out.3 kernels run.  More channels run the general conv kernels
+        # on NHWC images padded to cp = a multiple of 4 channels (zero image channels, zero weight columns / rows)
+        if in_channels < 1:
+            raise ValueError("in_channels must be >= 1")
+        self.cimg = in_channels
+        self.cp = 1 if in_channels == 1 else _cdiv(in_channels, 4) * 4
         self.conv_math = conv_math
         self.nterm = CONV_MATH[conv_math]
         # the 16-bit-MFMA kernel family with every train-mode fusion: h3 (fp32-class) and bf16 (C4 mixed precision)
@@ -159,7 +168,7 @@ class UNetEngine:
         # eval: the pool / FiLM / residual applies in the conv epilogue (fuses_eval)
         self.fuse_eval = self.x16 and os.environ.get("CDM_FUSE_EVAL", "1") != "0"
         self.device = torch.device(device)
-        self.layers = conv_layers(n_feat, height)
+        self.layers = conv_layers(n_feat, height, self.cp)
         self.L = {l.name: l for l in self.layers}
         self.KK0 = (height // 4) ** 2
         # up0 on large maps (config 5: k = 64, 1.07 G weights): VALU kernels over the weights in their reference layout
@@ -190,7 +199,7 @@ class UNetEngine:
         slots, max|W| per layer, the split images straight from OIHW (cdm_pack_split_conv3x3_batch; bf16: the one-term
         hi plane, round 5 — it replaced 40 split + 18 pack launches per C4 step)."""
         nf = self.nf
-        specs = [(l.name, P[l.w], l.cin, l.cout, l.kc) for l in self.layers if l.cin > 1]
+        specs = [(l.name, self._layer_w(P, l), l.cin, l.cout, l.kc) for l in self.layers if l.cin > 1]
         specs.append(("out.0", P["out.0.weight"], 2 * nf, nf, self.kc_out0))
         key = tuple(w.data_ptr() for _, w, *_ in specs)
         if self._batch_key != key:
@@ -228,9 +237,9 @@ class UNetEngine:
         if batched:
             self._repack_h3_train_batched(P, stream)
         for l in self.layers:
-            W, b = P[l.w], P[l.b]
             if batched and l.cin > 1:
                 continue
+            W, b = self._layer_w(P, l), P[l.b]
             if train:
                 wpk = self._buf(l.name + ".wpk", (9 * l.cin, l.cout))
                 wdg = (self._buf(l.name + ".wdg", (9 * l.cout, l.cin))) if l.cin > 1 else None
@@ -262,6 +271,22 @@ class UNetEngine:
             self._split("out.0.wpk", 9 * 2 * nf, nf, stream)
             if train:
                 self._split("out.0.wdg", 9 * nf, 2 * nf, stream)
+        if self.cp > 1:
+            # out.3 (n_feat -> in_channels) on the general conv kernels: weights / bias padded to cp output channels
+            cp, C = self.cp, self.cimg
+            w3 = self._buf("out.3.wpad", (cp, nf, 3, 3))
+            b3 = self._buf("out.3.bpad", (cp,))
+            w3[C:].zero_(); w3[:C].copy_(P["out.3.weight"])
+            b3[C:].zero_(); b3[:C].copy_(P["out.3.bias"])
+            self.pk["out.3.wpad"], self.pk["out.3.bpad"] = w3, b3
+            wpk = self._buf("out.3.wpk", (9 * nf, cp))
+            wdg = self._buf("out.3.wdg", (9 * cp, nf))
+            lb.cdm_pack_conv3x3(_p(w3), _p(b3), nf, cp, None, None, None, None, 0.0, _p(wpk), None,
+                                _p(wdg) if train else None, conv_kc(nf, cp), stream)
+            self.pk["out.3.wpk"], self.pk["out.3.wdg"] = wpk, wdg
+            self._split("out.3.wpk", 9 * nf, cp, stream)
+            if train:
+                self._split("out.3.wdg", 9 * cp, nf, stream)
         for name, cin in (("up1.model.0", 4 * nf), ("up2.model.0", 2 * nf)):
             wt = self._buf(name + ".wt", (cin, 4 * nf))
             wtT = self._buf(name + ".wtT", (4 * nf, cin))
@@ -288,6 +313,16 @@ class UNetEngine:
             lb.cdm_transpose(_p(w2), E, E, _p(w2t), stream)
             self.pk[m + ".w2t"] = w2t
         self._pk_key = (key, train) if key is not None else None
+
+    def _layer_w(self, P, l: "LayerSpec") -> torch.Tensor:
+        """Conv l's OIHW weights; the init conv's with zero columns for the padded image channels (in_channels > 1)."""
+        W = P[l.w]
+        if l is not self.layers[0] or self.cp == self.cimg:
+            return W
+        wp = self.pk["init.wpad"] = self._buf("init.wpad", (self.nf, self.cp, 3, 3))
+        wp[:, self.cimg:].zero_()
+        wp[:, :self.cimg].copy_(W)
+        return wp
 
     def invalidate(self):
         """Parameters changed behind torch's version counters (fused Adam): drop the cached eval pack."""
@@ -387,11 +422,11 @@ class UNetEngine:
         """out.1's GroupNorm + ReLU runs inside out.3's kernels (forward; train: and its weight gradient): zO is never
         written, and its workspace buffer is not allocated."""
         nf, H = self.nf, self.H
-        return (not train or self.fuse_gn_out) and nf % 16 == 0 and H <= 256 and 256 % H == 0
+        return (self.cp == 1 and (not train or self.fuse_gn_out) and nf % 16 == 0 and H <= 256 and 256 % H == 0)
 
     def fuses_bn_bwd(self, l: "LayerSpec", kind: str, B: int = 1) -> bool:
         """Layer l's BN backward runs inside its dgrad / wgrad staging (cdm_conv3x3_*_h3_bnbwd)."""
-        return (self.fuse_bn_bwd and kind in ("dense", "plain", "resid") and l.cin > 1
+        return (self.fuse_bn_bwd and kind in ("dense", "plain", "resid") and l.cin > 1 and l is not self.layers[0]
                 and l.S in ((32, 64, 128) if self.h3 else (32, 64))
                 and self.halo_addressable(B, l.S)
                 and l.kc == 16 and l.cin % 128 == 0 and l.cout % 128 == 0 and l.cout <= 256)
@@ -420,7 +455,10 @@ class UNetEngine:
                    "up1.model.1.conv1": "yT1", "up2.model.1.conv1": "yT2"}
         if l.name in special:
             return self._slot(ws, special[l.name])
-        prev = self.layers[self.layers.index(l) - 1]
+        i = self.layers.index(l)
+        if i == 0:
+            return None            # the image (in_channels > 1): its max is measured by the conv call
+        prev = self.layers[i - 1]
         return self._dst_slot(ws, prev)
 
     # ------------------------------------------------------------------------------------------
@@ -436,12 +474,13 @@ class UNetEngine:
     def forward(self, ws: "Workspace", P, x: torch.Tensor, t_in: torch.Tensor, c_in: Optional[torch.Tensor],
                 sc_w: torch.Tensor, sc_b: torch.Tensor, sc_split: int, stream: int, out: Optional[torch.Tensor] = None,
                 frozen: bool = False):
-        """x [B,H,W] fp32 (C=1, NCHW == NHWC), t_in [rows_t] (rows 1 or B), c_in [rows_c, ncf] or None (zeros).
+        """x [B,H,W] fp32 (C=1, NCHW == NHWC; in_channels > 1: NHWC [B*H*W, cp] with zero padding channels), t_in [rows_t]
+        (rows 1 or B), c_in [rows_c, ncf] or None (zeros).
 
         sc_w/sc_b: shortcut 1x1 conv weights, [2, nf] when sc_split < B (CFG halves) else [nf]-shaped.
         frozen (train-mode workspace only): BatchNorm with the running statistics, not updated — the forward of
         model.eval() kept for a backward (backward(..., frozen=True)).
-        Returns eps [B, H, W] (written into ``out`` when given)."""
+        Returns eps [B, H, W] (in_channels > 1: NHWC [B*H*W, cp]; written into ``out`` when given)."""
         lb = lib(); s = stream
         nf, H, B = self.nf, self.H, ws.B
         H1, H2 = H // 2, H // 4
@@ -451,6 +490,9 @@ class UNetEngine:
         ws.frozen = frozen
         eps = out if out is not None else ws.eps
         ws.x_in = x
+        if self.cp > 1:
+            assert x.numel() == B * H * H * self.cp
+            ws.src["init_conv.conv1"] = Act(x, self.cp)
         ws.sc_pending = (sc_w, sc_b, sc_split)
         if self.nterm == NT_H3:
             lb.cdm_zero_f32(_p(ws.amax), ws.amax.numel(), s)
@@ -535,8 +577,13 @@ class UNetEngine:
             ws.zO_fused = train
             return eps
         ws.zO_fused = False
+        zslot = self._slot(ws, "zO") if self.cp > 1 else None
         lb.cdm_norm_apply_fwd(APPLY_RELU, _p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]), _p(ws.gnO["shift"]), nf,
-                              None, 0, None, 0, None, None, None, 0, _p(ws.zO), nf, None, s)
+                              None, 0, None, 0, None, None, None, 0, _p(ws.zO), nf, zslot, s)
+        if self.cp > 1:   # out.3: n_feat -> in_channels (padded to cp) on the general conv kernels
+            self.conv3x3("out.3.wpk", _p(ws.zO), B, H, nf, nf, _p(self.pk["out.3.bpad"]), _p(eps), self.cp, self.cp, 0,
+                         None, 0, conv_kc(nf, self.cp), s, amax_x=zslot)
+            return eps
         lb.cdm_conv3x3_cout1_fwd(_p(ws.zO), nf, B, H, H, nf, _p(P["out.3.weight"]), _p(P["out.3.bias"]), _p(eps), s)
         return eps
 
@@ -626,6 +673,10 @@ class UNetEngine:
             lb.cdm_norm_apply_fwd(APPLY_FILM | relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), 0, _p(ce),
                                   C if ws.c_rows > 1 else 0, _p(te), C if ws.t_rows > 1 else 0, None, None, None, 0,
                                   dst.p, dst.ld, am, s)
+        elif kind == "resid" and self.cp > 1:
+            sc_w, sc_b, split = ws.sc_pending
+            lb.cdm_norm_apply_fwd_resid_c(relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), _p(x), self.cp, self.cimg,
+                                          _p(sc_w), _p(sc_b), split, dst.p, dst.ld, am, s)
         elif kind == "resid":
             sc_w, sc_b, split = ws.sc_pending
             lb.cdm_norm_apply_fwd(APPLY_RESID | relu, _p(y), C, B, S, S, C, _p(scale), _p(shift), 0, None, 0, None,
@@ -637,7 +688,7 @@ class UNetEngine:
         """Eval forward of a pool / FiLM / residual layer with its output transform in the LDS-halo conv's epilogue
         (cdm_conv3x3_fwd_x16_fused: 32^2 / 64^2 maps, 16-bit arithmetics); $CDM_FUSE_EVAL=0 keeps the apply kernel."""
         return (self.fuse_eval and l.cin > 1 and l.kc == 16 and l.S in (32, 64) and l.cout % 128 == 0
-                and self.halo_addressable(B, l.S))
+                and self.halo_addressable(B, l.S) and not (self.cp > 1 and l.name == "init_conv.conv2"))
 
     def _conv_eval_fused(self, ws, l: "LayerSpec", kind: str, x, s):
         lb = lib()
@@ -699,18 +750,21 @@ class UNetEngine:
         H1, H2 = H // 2, H // 4
         P0, P1, P2 = B * H * H, B * H1 * H1, B * H2 * H2
         # ---------------- out.3 (nf -> 1) ----------------
-        R = cout1_band_rows(B, H)
-        if ws.zO_fused:
-            lb.cdm_conv3x3_cout1_wgrad_gn(_p(deps), _p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]),
-                                          _p(ws.gnO["shift"]), -R, _p(ws.slab), s)
+        if self.cp > 1:
+            gO = self._out3_bwd_c(ws, deps, G, s)
         else:
-            lb.cdm_conv3x3_cout1_wgrad(_p(deps), _p(ws.zO), nf, B, H, H, nf, -R, _p(ws.slab), s)
-        S = fold(ws, _p(ws.slab), B * H // R, 9, nf, s)
-        lb.cdm_slab_sum_all(_p(ws.dpart), S, 9, 0, 9, nf, _p(G["out.3.weight"]), 1, 9, 0, s)
-        if not out3_bias_done:
-            _sum_into(deps, G["out.3.bias"], ws, s)
-        gO = ws.G0
-        lb.cdm_conv3x3_cout1_dgrad(_p(deps), B, H, H, nf, _p(P["out.3.weight"]), _p(gO), nf, s)
+            R = cout1_band_rows(B, H)
+            if ws.zO_fused:
+                lb.cdm_conv3x3_cout1_wgrad_gn(_p(deps), _p(ws.yO), nf, B, H, H, nf, _p(ws.gnO["scale"]),
+                                              _p(ws.gnO["shift"]), -R, _p(ws.slab), s)
+            else:
+                lb.cdm_conv3x3_cout1_wgrad(_p(deps), _p(ws.zO), nf, B, H, H, nf, -R, _p(ws.slab), s)
+            S = fold(ws, _p(ws.slab), B * H // R, 9, nf, s)
+            lb.cdm_slab_sum_all(_p(ws.dpart), S, 9, 0, 9, nf, _p(G["out.3.weight"]), 1, 9, 0, s)
+            if not out3_bias_done:
+                _sum_into(deps, G["out.3.bias"], ws, s)
+            gO = ws.G0
+            lb.cdm_conv3x3_cout1_dgrad(_p(deps), B, H, H, nf, _p(P["out.3.weight"]), _p(gO), nf, s)
         # ---------------- out.1 GroupNorm + ReLU ----------------
         dyO = ws.D0
         dslot = self._slot(ws, "dy:out.0")
@@ -802,8 +856,46 @@ class UNetEngine:
         hook("down1")
         self._chain_bwd(ws, P, self.layers[0:2], G, s)
         if dx is not None:
-            self._image_grad(ws, P, dx, s)
+            if self.cp > 1:
+                self._image_grad_c(ws, dx, s)
+            else:
+                self._image_grad(ws, P, dx, s)
         hook("init")
+
+    def _out3_bwd_c(self, ws, deps: torch.Tensor, G, s: int):
+        """out.3 = Conv2d(n_feat, in_channels > 1) backward on the general kernels; deps = dL/d eps, NHWC [B*H*W, cp] with
+        zero padding channels.  Returns the gradient wrt zO = relu(GN(yO)) (ws.G0)."""
+        lb = lib()
+        nf, H, B, cp, C = self.nf, self.H, ws.B, self.cp, self.cimg
+        zslot = self._slot(ws, "zO")
+        gw = self._buf("out.3.gwpad", (cp, nf, 3, 3))
+        self._wgrad3x3(ws, Act(deps, cp), Act(ws.zO, nf), B, H, nf, cp, gw, s, amax_x=zslot)
+        G["out.3.weight"].copy_(gw[:C])
+        gb = self._buf("out.3.gbpad", (cp,))
+        lb.cdm_reduce_sum(_p(deps), cp, B, H * H, cp, CHUNK, _p(ws.slab), s)
+        nparts = fold(ws, _p(ws.slab), B * _cdiv(H * H, CHUNK), 1, cp, s)
+        lb.cdm_slab_sum_all(_p(ws.dpart), nparts, 1, 0, 1, cp, _p(gb), 0, 1, 0, s)
+        G["out.3.bias"].copy_(gb[:C])
+        gO = ws.G0
+        self.conv3x3("out.3.wdg", _p(deps), B, H, cp, cp, None, _p(gO), nf, nf, 0, None, 0, conv_kc(cp, nf), s)
+        return gO
+
+    def _image_grad_c(self, ws, dx: torch.Tensor, s: int):
+        """dL/dx for in_channels > 1 (NHWC [B*H*W, cp]): init_conv.conv1's input gradient (its dgrad, already in
+        ws.dgrad_dst) plus the random 1x1 shortcut's, dx[p][k] += sum_n g_res[p][n] w[n][k] (one GEMM)."""
+        lb = lib()
+        nf, H, B, cp, C = self.nf, self.H, ws.B, self.cp, self.cimg
+        l = self.layers[0]
+        P0 = B * H * H
+        gd = ws.dgrad_dst[l.name]
+        dx.view(P0, cp).copy_(gd.buf.view(-1)[: P0 * gd.ld].view(P0, gd.ld)[:, :cp])
+        sc_w, _, split = ws.sc_pending
+        assert split >= B, "input gradients with two shortcut draws (CFG halves) are not a module-call form"
+        wpad = self._buf("sc.wpad", (nf, cp))
+        wpad[:, C:].zero_(); wpad[:, :C].copy_(sc_w[: nf * C].view(nf, C))
+        gres = ws.gout["init_conv.conv2"]
+        sp = lib().raw("cdm_gemm_splits")(nf, 1)
+        lb.cdm_gemm_f32(gres.p, gres.ld, P0, nf, _p(wpad), cp, cp, _p(dx), cp, None, 1, EPI_ACCUM, sp, _p(ws.slab), s)
 
     def _image_grad(self, ws, P, dx: torch.Tensor, s: int):
         """dL/dx of the image (ResidualConvBlock(1, nf, is_res) at diffusion_utilities.py:45-55 under autograd):
@@ -938,8 +1030,12 @@ class UNetEngine:
         self.conv3x3(l.name + ".wdg", dy.p, B, S, C, dy.ld, None, dgd.p, dgd.ld, l.cin,
                      EPI_ACCUM if ws.dgrad_accum[l.name] else 0, None, 0, l.kc, s, amax_x=dslot, amax_y=gslot,
                      dt=self._dgrad_out16(ws, l))
-        self._wgrad3x3(ws, dy, src, B, S, l.cin, C, G[l.w], s, amax_dy=dslot, amax_x=self._src_slot(ws, l), pre=pre,
+        pad0 = l is self.layers[0] and self.cp > self.cimg      # the init conv's zero image-channel columns
+        gW = self._buf("init.gwpad", (C, self.cp, 3, 3)) if pad0 else G[l.w]
+        self._wgrad3x3(ws, dy, src, B, S, l.cin, C, gW, s, amax_dy=dslot, amax_x=self._src_slot(ws, l), pre=pre,
                        sums_of=l)
+        if pad0:
+            G[l.w].copy_(gW[:, :self.cimg])
 
     def _src_pre(self, ws, l: "LayerSpec"):
         """(input activation, BN-ReLU transform or None) of conv l in train mode: a fused producer hands over its
@@ -1138,7 +1234,7 @@ class Workspace:
         self.catO = Act(E(P0, 2 * nf), 2 * nf)
         self.catU2 = Act(E(P1, 2 * nf), 2 * nf)
         self.catU1 = Act(E(P2, 4 * nf), 4 * nf)
-        self.eps = E(B, H, H)
+        self.eps = E(B, H, H) if eng.cp == 1 else E(P0, eng.cp)
         self.yT1 = E(P1, nf)
         self.yT2 = E(P0, nf)
         self.y0 = E(P2, 2 * nf)
@@ -1338,6 +1434,8 @@ class Workspace:
                     need = max(need, sp * l.cout * 9 * l.cin)
             # out.0 (2nf -> nf at full resolution; not in eng.layers)
             need = max(need, wgrad_splits(P0, nf, 9 * 2 * nf) * nf * 9 * 2 * nf)
+            if eng.cp > 1:                                  # out.3 (nf -> in_channels) on the general weight gradient
+                need = max(need, wgrad_splits(P0, eng.cp, 9 * nf) * eng.cp * 9 * nf)
             for cin, Hin in ((4 * nf, H // 4), (2 * nf, H // 2)):   # convT wgrad
                 need = max(need, wgrad_splits(B * Hin * Hin, cin, 4 * nf) * cin * 4 * nf)
             if not (eng.up0_large and B <= 16):             # up0 weight grad through a split-K slab

@@ -110,13 +110,13 @@ _ENGINES: Dict[tuple, UNetEngine] = {}
 _MODEL_UIDS = itertools.count()
 
 
-def get_engine(n_feat, n_cfeat, height, device, conv_math: str = "fp32") -> UNetEngine:
+def get_engine(n_feat, n_cfeat, height, device, conv_math: str = "fp32", in_channels: int = 1) -> UNetEngine:
     dev = torch.device(device)
     key = (n_feat, n_cfeat, height, dev.type, dev.index if dev.index is not None else torch.cuda.current_device(),
-           conv_math)
+           conv_math, in_channels)
     eng = _ENGINES.get(key)
     if eng is None:
-        eng = _ENGINES[key] = UNetEngine(n_feat, n_cfeat, height, dev, conv_math)
+        eng = _ENGINES[key] = UNetEngine(n_feat, n_cfeat, height, dev, conv_math, in_channels)
     return eng
 
 
@@ -136,20 +136,20 @@ class _UNetFunction(torch.autograd.Function):
     def forward(ctx, holder, x, t, c, sc_w, sc_b, *params):
         mod: "ContextUnet" = holder[0]
         frozen = holder[1]          # eval mode: BatchNorm on the running statistics (batch_norm(training=False))
-        eng, P = mod._engine_and_params()
+        eng, P = mod._engine_and_params(image_channels_ok=True)
         s = _stream()
         B = x.shape[0]
         eng.repack(P, True, s)
         ctx.pack_token = eng.train_pack_token = object()   # whose weights the engine's train pack holds
         ws = eng.workspace(B, True, frozen=frozen)
-        eps = eng.forward(ws, P, x.reshape(B, mod.h, mod.h), t, c, sc_w, sc_b, B, s, frozen=frozen)
+        eps = eng.forward(ws, P, mod._to_engine(x), t, c, sc_w, sc_b, B, s, frozen=frozen)
         ctx.frozen = frozen
         mod._invalidate_eval_pack()
         ctx.state = (mod, eng, ws, P)
         # the engine backward reads the live parameters (BatchNorm weights, ConvT / EmbedFC weights): saved so that
         # autograd's version check raises if one was updated in place between forward and backward
         ctx.save_for_backward(*params)
-        return eps.view(B, 1, mod.h, mod.h)
+        return mod._from_engine(eps, B)
 
     @staticmethod
     def backward(ctx, geps):
@@ -164,14 +164,14 @@ class _UNetFunction(torch.autograd.Function):
         G = {n: torch.empty_like(P[n]) for n in names}
         dev = geps.device
         need_x, need_t, need_c = ctx.needs_input_grad[1:4]
-        dx = torch.empty(ws.B, mod.h, mod.h, device=dev) if need_x else None
+        dx = torch.empty(ws.B * mod.h * mod.h * eng.cp, device=dev) if need_x else None
         dt = torch.empty(ws.t_rows, device=dev) if need_t else None
         dc = torch.empty(ws.c_rows, mod.n_cfeat, device=dev) if need_c else None
         ws.frozen = ctx.frozen
-        eng.backward(ws, P, geps.reshape(ws.B, mod.h, mod.h).contiguous(), G, _stream(), dx=dx, dt=dt, dc=dc)
+        eng.backward(ws, P, mod._to_engine(geps), G, _stream(), dx=None if dx is None else dx.view_as(ws.eps), dt=dt,
+                     dc=dc)
         ctx.state = None
-        return (None, None if dx is None else dx.view(ws.B, 1, mod.h, mod.h), dt, dc, None, None,
-                *[G[n] for n in names])
+        return (None, None if dx is None else mod._from_engine(dx, ws.B), dt, dc, None, None, *[G[n] for n in names])
 
 
 class ContextUnet(nn.Module):
@@ -208,9 +208,13 @@ class ContextUnet(nn.Module):
         self._sc_counter = 0
 
     # -------------------------------------------------------------------------------------------
-    def _engine_and_params(self):
-        if self.in_channels != 1:
-            raise NotImplementedError("the HIP path implements the reference's in_channels=1 maps")
+    def _engine_and_params(self, image_channels_ok: bool = False):
+        """(engine, parameters).  Module calls (forward / backward) take any in_channels; the reference's training loop,
+        samplers and likelihood are single-channel (train_diffusion_condition.py:101,301 build in_channels = 1 and draw
+        [n, 1, H, W]), and so are this package's graph-captured versions of them."""
+        if self.in_channels != 1 and not image_channels_ok:
+            raise NotImplementedError("the training loop / samplers / likelihood of the reference (and of this package) "
+                                      "are single-channel: ContextUnet(in_channels > 1) runs module calls only")
         P = dict(self.named_parameters())
         P.update(dict(self.named_buffers()))
         dev = P["out.3.weight"].device
@@ -221,7 +225,27 @@ class ContextUnet(nn.Module):
                 continue
             if v.dtype != torch.float32 or not v.is_contiguous():
                 raise RuntimeError(f"{k}: expected contiguous fp32 (got {v.dtype})")
-        return get_engine(self.n_feat, self.n_cfeat, self.h, dev, self.conv_math), P
+        return get_engine(self.n_feat, self.n_cfeat, self.h, dev, self.conv_math, self.in_channels), P
+
+    def _to_engine(self, x: torch.Tensor) -> torch.Tensor:
+        """[B, C, H, W] -> the engine's image layout: [B, H, W] for C = 1 (NCHW == NHWC); NHWC [B*H*W, cp] with zero
+        channels up to cp = a multiple of 4 otherwise."""
+        B, C, h = x.shape[0], self.in_channels, self.h
+        if tuple(x.shape[1:]) != (C, h, h):
+            raise ValueError(f"expected x of shape [B, {C}, {h}, {h}], got {tuple(x.shape)}")
+        if C == 1:
+            return x.reshape(B, h, h).contiguous()
+        cp = (C + 3) // 4 * 4
+        xe = x.new_zeros(B, h, h, cp)
+        xe[..., :C] = x.permute(0, 2, 3, 1)
+        return xe.view(B * h * h, cp)
+
+    def _from_engine(self, e: torch.Tensor, B: int) -> torch.Tensor:
+        """the engine's image layout -> [B, C, H, W] (inverse of _to_engine)"""
+        C, h = self.in_channels, self.h
+        if C == 1:
+            return e.view(B, 1, h, h)
+        return e.view(B, h, h, -1)[..., :C].permute(0, 3, 1, 2).contiguous()
 
     def _invalidate_eval_pack(self):
         self._eval_key = None
@@ -233,25 +257,31 @@ class ContextUnet(nn.Module):
         return (self._uid,) + tuple((v.data_ptr(), v._version) for v in P.values())
 
     def draw_shortcut(self, device, n_sets: int = 1):
-        """Fresh 1x1 shortcut (diffusion_utilities.py:54).  Returns (w [n_sets*nf], b [n_sets*nf])."""
+        """Fresh 1x1 shortcut (diffusion_utilities.py:54).  Returns (w [n_sets*nf*in_channels], b [n_sets*nf])."""
         nf = self.n_feat
+        if self.in_channels == nf:
+            # diffusion_utilities.py:50-52: same channels -> out = x + x2, no 1x1 conv is built (no RNG draw); the
+            # identity weights make the residual apply compute exactly that
+            eye = torch.eye(nf, device=device).reshape(-1)
+            return eye.repeat(n_sets), torch.zeros(n_sets * nf, device=device)
         if self.shortcut_source == "cpu":
             ws, bs = [], []
             for _ in range(n_sets):
                 conv = nn.Conv2d(self.in_channels, nf, kernel_size=1, stride=1, padding=0)
-                ws.append(conv.weight.detach().reshape(nf)); bs.append(conv.bias.detach())
+                ws.append(conv.weight.detach().reshape(-1)); bs.append(conv.bias.detach())
             return torch.cat(ws).to(device), torch.cat(bs).to(device)
         from ._lib import lib
-        w = torch.empty(2 * n_sets * nf, device=device)
+        nw = n_sets * nf * self.in_channels
+        w = torch.empty(nw + n_sets * nf, device=device)
         self._sc_counter += 1
         lib().cdm_philox_uniform(w.data_ptr(), w.numel(), -1.0, 1.0, 0x5C0FFEE + id(self) % 65536,
                                  self._sc_counter, None, _stream())
-        return w[: n_sets * nf], w[n_sets * nf:]
+        return w[:nw], w[nw:]
 
     # -------------------------------------------------------------------------------------------
     def forward(self, x, t, c=None):
-        """x [B,1,H,W]; t in [0,1] with B or 1 elements (any shape); c [B|1, n_cfeat] or None (zeros)."""
-        eng, P = self._engine_and_params()
+        """x [B,in_channels,H,W]; t in [0,1] with B or 1 elements (any shape); c [B|1, n_cfeat] or None (zeros)."""
+        eng, P = self._engine_and_params(image_channels_ok=True)
         dev = x.device
         B = x.shape[0]
         x = x.to(torch.float32).contiguous()
@@ -276,9 +306,11 @@ class ContextUnet(nn.Module):
             key = self._eval_pack_key(P)
             eng.repack(P, False, s, key=key)
         ws = _cached_ws(eng, B, train)
-        eps = torch.empty(B, 1, self.h, self.h, device=dev)
-        eng.forward(ws, P, x.reshape(B, self.h, self.h), t, c, sc_w, sc_b, B, s, out=eps.view(B, self.h, self.h))
-        return eps
+        if self.in_channels == 1:
+            eps = torch.empty(B, 1, self.h, self.h, device=dev)
+            eng.forward(ws, P, self._to_engine(x), t, c, sc_w, sc_b, B, s, out=eps.view(B, self.h, self.h))
+            return eps
+        return self._from_engine(eng.forward(ws, P, self._to_engine(x), t, c, sc_w, sc_b, B, s), B)
 
 
 _WS: Dict[tuple, object] = {}

@@ -299,6 +299,12 @@ int cdm_col_sum3(const float* in0, float* out0, const float* in1, float* out1, c
 int cdm_norm_apply_fwd(int flags, const float* y, int ldy, int N, int H, int W, int C, const float* s, const float* t,
                        int sn, const float* film_a, int film_an, const float* film_b, int film_bn, const float* rx,
                        const float* rw, const float* rb, int rsplit, float* out, int ldo, float* amax, void* stream);
+/* the same residual apply for in_channels = xc > 1 (ContextUnet.py:6,14 — init_conv = ResidualConvBlock(in_channels,
+ * n_feat, is_res=True), the 1x1 shortcut of diffusion_utilities.py:54-55 over xc channels):
+ * out = [relu](y*s+t) + rb[c] + sum_k rw[c][k] rx[p*ldx + k]; rw [2][C][xc] / rb [2][C] when rsplit < N */
+int cdm_norm_apply_fwd_resid_c(int relu, const float* y, int ldy, int N, int H, int W, int C, const float* s,
+                               const float* t, const float* rx, int ldx, int xc, const float* rw, const float* rb,
+                               int rsplit, float* out, int ldo, float* amax, void* stream);
 int cdm_norm_apply_bwd(int mode, const float* g, int ldg, const float* y, int ldy, int N, int H, int W, int C,
                        const float* s, const float* t, int sn, const float* mean, const float* invstd, int mn, int cpg,
                        const float* film_a, int film_an, const float* A, const float* B, const float* Cc, int cn,

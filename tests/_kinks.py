@@ -59,13 +59,13 @@ def hip_kinks(m, x, t, c, sc, frozen):
     kernels of the module call): per ReLU the mask of z = fma(y, s, t) > 0 (NCHW) and z, per MaxPool the first-max index
     of relu(z) over each window (the pool apply's order).  Call order: the 10 encoder Conv-BN-ReLU layers (a pool after
     the 6th and the 10th), up0's GroupNorm-ReLU, the 8 decoder layers, out.1's GroupNorm-ReLU."""
-    eng, P = m._engine_and_params()
+    eng, P = m._engine_and_params(image_channels_ok=True)
     NF, H, B = m.n_feat, m.h, x.shape[0]
     s = torch.cuda.current_stream().cuda_stream
     eng.repack(P, True, s)
     ws = eng.workspace(B, True, frozen=frozen)
-    eng.forward(ws, P, x.cuda().reshape(B, H, H), t.cuda(), c.cuda(), sc[0].reshape(-1).cuda(), sc[1].cuda(), B, s,
-                frozen=frozen)
+    eng.forward(ws, P, m._to_engine(x.cuda().reshape(B, m.in_channels, H, H)), t.cuda(), c.cuda(),
+                sc[0].reshape(-1).cuda(), sc[1].cuda(), B, s, frozen=frozen)
     torch.cuda.synchronize()
 
     def z_of(y, scale, shift, C, S, per_sample):

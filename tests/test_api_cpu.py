@@ -102,3 +102,37 @@ def test_cpu_blocks_fail_loudly():
     blk = ResidualConvBlock(4, 8)
     blk.set_out_channels(16)                      # diffusion_utilities.py:72-75: attributes only
     assert blk.conv1[0].out_channels == blk.conv2[0].in_channels == blk.conv2[0].out_channels == 16
+
+
+def test_in_channels_layout_and_shortcut_draws():
+    """ContextUnet(in_channels > 1): the reference's state_dict layout, the engine's padded image channels (layer specs
+    and the NHWC image layout, round-tripped), and the shortcut draws — a fresh Conv2d(C, n_feat, 1) from the CPU RNG
+    (the same draws as the reference's), none at all when in_channels == n_feat (identity, diffusion_utilities.py:50-52)."""
+    import torch
+    import cdm_amd
+    from cdm_amd import engine as E
+    from oracle import ref_cpu as R
+    m = cdm_amd.ContextUnet(3, 16, 6, 16)
+    lay = R.state_dict_layout(3, 16, 6, 16)
+    sd = m.state_dict()
+    assert [k for k, *_ in lay] == list(sd.keys())
+    assert all(tuple(sd[k].shape) == tuple(shp) for k, shp, _ in lay)
+    L = E.conv_layers(16, 16, 4)
+    assert (L[0].cin, L[0].kc, L[1].cin) == (4, 0, 16)
+    x = torch.randn(2, 3, 16, 16)
+    xe = m._to_engine(x)
+    assert xe.shape == (2 * 16 * 16, 4) and torch.equal(xe[:, 3], torch.zeros(512))
+    assert torch.equal(m._from_engine(xe, 2), x)
+    torch.manual_seed(4)
+    w, b = m.draw_shortcut("cpu")
+    torch.manual_seed(4)
+    rw, rb = R.draw_shortcut(3, 16)
+    assert torch.equal(w, rw.reshape(-1)) and torch.equal(b, rb)
+    same = cdm_amd.ContextUnet(16, 16, 6, 16)
+    state = torch.get_rng_state()
+    w, b = same.draw_shortcut("cpu")
+    assert torch.equal(torch.get_rng_state(), state)
+    assert torch.equal(w, torch.eye(16).reshape(-1)) and not b.any()
+    import pytest
+    with pytest.raises(NotImplementedError):
+        m._engine_and_params()            # training loop / samplers: single-channel only

@@ -32,7 +32,10 @@ NF, NCF, H, B, T, LR = 128, 6, 64, 256, 1500, 1e-5
 def _gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    old = torch.get_num_threads()
     torch.set_num_threads(min(16, max(1, len(__import__("os").sched_getaffinity(0)))))
+    yield
+    torch.set_num_threads(old)
 
 
 def _bn_fed_bias(k):
