@@ -10,6 +10,10 @@ network barely amplifies).  Train-mode BatchNorm, n_feat = 16, B = 4, input seed
 no arithmetic flips a decision; round 5's audit, tools/kink_diag.py / profiles/r5_kink_diag.txt, found HIP's per-layer
 pre-activation errors equal to or below the reference's on every layer — the flips are single elements at |z| below
 the rounding error, which either arithmetic takes by chance, and the strict bar per branch needs no seed selection).
+BatchNorm weight / bias gradients under h3 add kappa * 2^-26 (kappa = the sum's condition number over pixels): the
+fp16 matrix cores' fp32 accumulation carries a small negative mean bias (profiles/r5_mfma_round_probe.jsonl) that a
+cancelling sum amplifies by kappa — in eval mode, where xhat uses the running statistics, kappa reaches 634
+(tools/eval_dgamma_diag.py).
 """
 import numpy as np
 import pytest
@@ -29,6 +33,9 @@ def _gpu():
 
 
 NF, NCF, H, B = 16, 6, 64, 4
+# relative bias floor of a gradient computed through the h3 convs: 2^-26 = 1.5e-8, 2.3x the largest accumulation bias
+# the fp16 matrix cores showed (profiles/r5_mfma_round_probe.jsonl, mean error -6.4e-9 of |C|)
+H3_ACC_BIAS = 2.0 ** -26
 
 
 def _rel_l2(a, b):
@@ -36,9 +43,11 @@ def _rel_l2(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
 
 
-def _oracle(sd, x, t, c, sc, dtype, weight, train=True, kinks=None):
+def _oracle(sd, x, t, c, sc, dtype, weight, train=True, kinks=None, kappa=None):
     """autograd of the oracle forward (train / eval BatchNorm) -> (eps, dx, dt, dc, param grads); kinks: a _Kinks
-    context (capture or impose)"""
+    context (capture or impose).  kappa (a dict): filled with the condition number of each BatchNorm weight / bias
+    gradient as a sum over pixels, ||sum_p |g xhat| || / ||sum_p g xhat|| (|| || over channels; g = the gradient at the
+    BatchNorm output, xhat its normalised input)."""
     sd = {k: (v.to(dtype) if v.is_floating_point() else v.clone()).clone() for k, v in sd.items()}
     keys = [k for k, _, kind in R.state_dict_layout(1, NF, NCF, H) if kind == "param"]
     for k in keys:
@@ -47,14 +56,42 @@ def _oracle(sd, x, t, c, sc, dtype, weight, train=True, kinks=None):
     tt = t.to(dtype).clone().requires_grad_(True)
     cc = c.to(dtype).clone().requires_grad_(True)
     import contextlib
-    with (kinks if kinks is not None else contextlib.nullcontext()):
-        eps = R.unet_forward(sd, xx, tt, cc, n_feat=NF, n_cfeat=NCF, height=H, train=train,
-                             shortcut=(sc[0].to(dtype), sc[1].to(dtype)))
+    rec = {}
+    orig_bn = R.F.batch_norm
+    bn_of = {id(sd[k]): k[: -len(".weight")] for k in keys if k.endswith(".1.weight")}
+
+    def bn(inp, rm, rv, w=None, b=None, training=False, momentum=0.1, eps=1e-5):
+        out = orig_bn(inp, rm, rv, w, b, training, momentum, eps)
+        name = bn_of.get(id(w))
+        if name is not None and out.requires_grad:
+            if training:
+                mean, var = inp.detach().mean((0, 2, 3)), inp.detach().var((0, 2, 3), unbiased=False)
+            else:
+                mean, var = rm.detach().clone(), rv.detach().clone()
+            rec[name] = [inp.detach(), mean, var, eps]
+            out.register_hook(lambda g_, n=name: rec[n].append(g_.detach()))
+        return out
+    if kappa is not None:
+        R.F.batch_norm = bn
+    try:
+        with (kinks if kinks is not None else contextlib.nullcontext()):
+            eps = R.unet_forward(sd, xx, tt, cc, n_feat=NF, n_cfeat=NCF, height=H, train=train,
+                                 shortcut=(sc[0].to(dtype), sc[1].to(dtype)))
+    finally:
+        R.F.batch_norm = orig_bn
     (eps * weight.to(dtype)).sum().backward()
+    for name, (y, mean, var, e, *gg) in rec.items():
+        if not gg:
+            continue
+        xh = (y - mean[None, :, None, None]) / torch.sqrt(var[None, :, None, None] + e)
+        gx = gg[0] * xh
+        kappa[name + ".weight"] = (gx.abs().sum((0, 2, 3)).norm() / gx.sum((0, 2, 3)).norm().clamp_min(1e-300)).item()
+        kappa[name + ".bias"] = (gg[0].abs().sum((0, 2, 3)).norm()
+                                 / gg[0].sum((0, 2, 3)).norm().clamp_min(1e-300)).item()
     return eps.detach(), xx.grad, tt.grad, cc.grad, {k: sd[k].grad for k in keys}
 
 
-def _branch_check(tag, m, sd, inputs, hip_grads, train, rec):
+def _branch_check(tag, m, sd, inputs, hip_grads, train, rec, acc_bias=0.0):
     """HIP's gradients vs fp64 autograd of the oracle on HIP's own branch (its ReLU / MaxPool decisions imposed) and the
     reference's fp32 gradients vs fp64 on the reference's branch (the larger error of its runs on this host's threads and
     on one thread, per tensor): a ReLU / MaxPool decision at |z| of the rounding error
@@ -67,7 +104,9 @@ def _branch_check(tag, m, sd, inputs, hip_grads, train, rec):
     _oracle(sd, x, t, c, sc, torch.float64, weight, train, cap64)
     hk_relu, hk_pool = hip_kinks(m, x, t, c, sc, frozen=not train)
     assert len(hk_relu) == len(cap64.relu) == 20 and len(hk_pool) == len(cap64.pool) == 2
-    e64h, dx64h, dt64h, dc64h, g64h = _oracle(sd, x, t, c, sc, torch.float64, weight, train, Kinks(hk_relu, hk_pool))
+    kappa = {}
+    e64h, dx64h, dt64h, dc64h, g64h = _oracle(sd, x, t, c, sc, torch.float64, weight, train, Kinks(hk_relu, hk_pool),
+                                              kappa)
     # the reference's own fp32 error: its run on this host's threads and its run on one thread (torch's CPU reductions
     # — batch-norm sums, weight-gradient sums over pixels — add in another order), each vs fp64 on its own branch; the
     # per-tensor larger of the two is the envelope HIP is held to (one fp32 run's error on a cancelling reduction, e.g.
@@ -111,9 +150,14 @@ def _branch_check(tag, m, sd, inputs, hip_grads, train, rec):
             continue
         eh, er = _rel_l2(hip, r64h), max(_rel_l2(r32, r64r), _rel_l2(r32_1, r64_1))
         rec[name] = (eh, er)
-        worst = max(worst, eh / (3 * er + 2e-6))
-        if eh > 3 * er + 2e-6:
-            bad.append((name, eh, er))
+        # a BatchNorm weight / bias gradient is a sum over pixels with condition number kappa: a systematic relative
+        # bias of its terms is amplified by kappa.  The fp16 matrix cores accumulate with a small negative bias (-1.5e-9
+        # .. -6.4e-9 of |C| in profiles/r5_mfma_round_probe.jsonl; the fp32 and bf16 MFMAs show none), which the h3
+        # dgrads pass on to g: floor kappa * acc_bias
+        bar = 3 * er + 2e-6 + kappa.get(name, 0.0) * acc_bias
+        worst = max(worst, eh / bar)
+        if eh > bar:
+            bad.append((name, eh, er, kappa.get(name)))
     print(f"[{tag}] decisions flipped vs fp64: HIP {flips_h}, reference fp32 {flips_r}; worst ratio {worst:.2f}; "
           f"worst", sorted(rec.items(), key=lambda kv: -kv[1][0])[:3])
     _parity.record("input_grads_branch", tag=tag, flips_hip=flips_h, flips_ref32=flips_r, worst_ratio=worst,
@@ -149,7 +193,8 @@ def test_input_grads_vs_autograd(math, bcast, seed):
     # the engine forward of _hip_kinks runs on the state before the module call (train mode: batch statistics; the
     # running statistics it updates again are not read)
     m.load_state_dict(sd)
-    _branch_check(f"{math}/{'b' if bcast else 's'}/seed{seed}", m, sd, (x, t, c, sc, weight), hip, True, {})
+    _branch_check(f"{math}/{'b' if bcast else 's'}/seed{seed}", m, sd, (x, t, c, sc, weight), hip, True, {},
+                  acc_bias=H3_ACC_BIAS if math == "h3" else 0.0)
     m.load_state_dict(sd_after)
 
 
@@ -284,4 +329,5 @@ def test_eval_mode_grads_vs_autograd(math, seed):
         if "running" in k or "num_batches" in k:
             assert torch.equal(v.cpu(), sd[k]), k
     hip = (eps.detach(), xg.grad.view(B, 1, H, H), tg.grad, cg.grad, {k: p.grad for k, p in m.named_parameters()})
-    _branch_check(f"eval/{math}/seed{seed}", m, sd, (x, t, c, sc, weight), hip, False, {})
+    _branch_check(f"eval/{math}/seed{seed}", m, sd, (x, t, c, sc, weight), hip, False, {},
+                  acc_bias=H3_ACC_BIAS if math == "h3" else 0.0)

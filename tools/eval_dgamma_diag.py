@@ -49,6 +49,15 @@ def run_box(out):
         sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
         kept = {}
         orig = E.UNetEngine.backward
+        orig_gn = E.UNetEngine._gn_bwd
+
+        def gn_bwd(self, ws, P, name, *a, **kw):   # dyO = dL/d out.0's output, right after out.1's GroupNorm backward
+            r = orig_gn(self, ws, P, name, *a, **kw)
+            if name == "out.1":
+                torch.cuda.synchronize()
+                kept["dyO"] = ws.D0.view(-1)[: ws.B * H * H * NF].detach().cpu().clone()
+            return r
+        E.UNetEngine._gn_bwd = gn_bwd
 
         def bwd(self, ws, *a, **kw):
             r = orig(self, ws, *a, **kw)
@@ -64,6 +73,8 @@ def run_box(out):
             (eps * weight.cuda()).sum().backward()
         finally:
             E.UNetEngine.backward = orig
+            E.UNetEngine._gn_bwd = orig_gn
+        res[math + "_dyO"] = kept["dyO"].numpy()
         gr = {k: p.grad.detach().cpu() for k, p in m.named_parameters()}
         res[math + "_y"] = kept["y"].numpy()
         res[math + "_g"] = kept["g"].numpy()
@@ -96,8 +107,19 @@ def analyse(path):
             if out.requires_grad:
                 out.register_hook(lambda gr_, k=k: rec[k].__setitem__("gbn", gr_.detach().clone()))
             return out
+        conv_rec = {}
+        orig_conv = F.conv2d
+
+        def conv(inp, w, b=None, stride=1, padding=0, *a):
+            out = orig_conv(inp, w, b, stride, padding, *a)
+            if tuple(w.shape) == (NF, 2 * NF, 3, 3) and out.requires_grad:     # out.0
+                conv_rec["w"] = w.detach().clone()
+                out.register_hook(lambda gr_: conv_rec.__setitem__("dyO", gr_.detach().clone()))
+            return out
+
         def run(dtype, kinks):
             rec.clear()
+            R.F.conv2d = conv
             s = {k: (v.to(dtype) if v.is_floating_point() else v.clone()).clone() for k, v in sd.items()}
             for k, v in s.items():
                 if v.is_floating_point() and "running" not in k:
@@ -110,6 +132,7 @@ def analyse(path):
                 (e * weight.to(dtype)).sum().backward()
             finally:
                 R.F.batch_norm = orig
+                R.F.conv2d = orig_conv
             return dict(rec), {k: v.grad for k, v in s.items() if v.grad is not None}
         cap = Kinks()
         r32, g32 = run(torch.float32, cap)
@@ -142,6 +165,15 @@ def analyse(path):
               f" corr with xhat {(eg * xh64).sum().item() / (eg.norm() * xh64.norm()).item():+.4f}")
         per = ((eg * xh64).sum((0, 2, 3)) / dgam64.abs().clamp_min(1e-300))
         print("   per-channel dgamma error from g:", " ".join(f"{v:+.1e}" for v in per.tolist()))
+        if math + "_dyO" in d.files:
+            dyo64 = conv_rec["dyO"]                                   # NCHW fp64 (HIP's branch)
+            dyoh = torch.from_numpy(d[math + "_dyO"]).double().reshape(B, H, H, NF).permute(0, 3, 1, 2)
+            w0 = conv_rec["w"].double()
+            # g wrt out.0's input recomputed in fp64 from HIP's dyO: the first n_feat channels are g of this layer
+            gi = torch.nn.grad.conv2d_input((B, 2 * NF, H, H), w0, dyoh, padding=1)[:, :NF] * (zh > 0)
+            print(f"   dyO rel {rel(dyoh, dyo64):.2e}; dgamma from fp64 dgrad of HIP's dyO "
+                  f"{rel((gi * xh64).sum((0, 2, 3)), dgam64):.2e}; HIP dgrad vs fp64 dgrad of HIP's dyO {rel(gh, gi):.2e},"
+                  f" dgamma from that dgrad error {rel(((gh - gi) * xh64).sum((0, 2, 3)) + dgam64, dgam64):.2e}")
 
 
 if __name__ == "__main__":
