@@ -596,7 +596,7 @@ def main():
     sample_ips = world * n / (sms * 1e-3 * T)
     _progress(f"C2 sample w=0 {sms:.3f} ms/step")
     cfg = {}
-    for w in (1.0, 3.0):
+    for w in ((1.0, 3.0) if args.cfg_sample_steps > 0 else ()):   # 0: no CFG legs (profiling runs)
         cms, CS = sample_rate(model, T, n, w, args.cfg_sample_steps, rank, barrier, dist)
         _progress(f"C2 sample w={w:g} {cms:.3f} ms/step")
         cfg[f"w={w:g}"] = {"ms_per_denoise_step": round(cms, 3), "steps_run": CS,

@@ -83,7 +83,8 @@ class Schedule:
         # denoise: (1 - a_t[t]) / (1 - ab_t[t]).sqrt() and a_t[t].sqrt() (0-d forms), b_t.sqrt()[t] (vector form);
         # fp32 subtraction / division in numpy: IEEE like torch's
         oma = (1 - a_t).numpy()
-        self.coef = torch.from_numpy((oma / sqrt_scalar_f32(1 - ab_t).numpy()).astype(np.float32)).to(dev)
+        with np.errstate(divide="ignore", invalid="ignore"):   # entry 0 (1 - ab_t[0] = 0) is never used: t >= 1
+            self.coef = torch.from_numpy((oma / sqrt_scalar_f32(1 - ab_t).numpy()).astype(np.float32)).to(dev)
         self.sa = sqrt_scalar_f32(a_t).to(dev)
         if sb is not None:
             sb = torch.as_tensor(sb).detach().to("cpu", torch.float32).reshape(-1)
