@@ -1674,7 +1674,13 @@ static __device__ __forceinline__ int trswz(int row, int ch) {   // byte offset 
     return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
 }
 
-template <int NT, int KS = 1>   // KS = 2 measured neutral (1.06 vs 1.07 ms per 309 GF)
+// CT (round 5): the ConvTranspose2d(k = 2, s = 2) weight gradient on the same staging (diffusion_utilities.py:86):
+// dW[ci][ij][co] = sum_{n,h,w} X[n,h,w][ci] dY[n,2h+i,2w+j][co] — "dy" is then the ConvT input X (rows M = its
+// channels), "x" its output gradient dY read at the sub-pixel (i, j) = (tap >> 1, tap & 1) of each input pixel (N =
+// 4 taps x its channels), H / W the input grid; the slab layout [z][ci][ij * Cout + co] of cdm_convT2x2_wgrad.  Both
+// operands are staged pixel-major as they arrive and read transposed, instead of the generic GEMM's 8 scalar
+// k-strided loads per column (0.19 of the h3 ceiling, round 4).
+template <int NT, int KS = 1, bool CT = false>   // KS = 2 measured neutral (1.06 vs 1.07 ms per 309 GF)
 __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float* __restrict__ dy, int lddy, int Cout,
                                                                      const float* __restrict__ x, int H, int W, int Cin,
                                                                      int ldx, int K, int kt_per_split,
@@ -1688,7 +1694,8 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
     const int wm = wave >> 1, wn = wave & 1;
     // 1-D grid, split-major logical order L = z*T + tile, remapped so that each XCD (hardware block b -> XCD b%8)
     // runs a contiguous range of L: the T tiles of one split share their dY / X pixel range in that XCD's L2.
-    const int gx = Cout / GBM, T = gx * (9 * Cin / GBN);
+    constexpr int NTAP = CT ? 4 : 9;
+    const int gx = Cout / GBM, T = gx * (NTAP * Cin / GBN);
     int L;
     {
         const int nwg = gridDim.x, q8 = nwg >> 3, r8 = nwg & 7, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
@@ -1698,6 +1705,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
     const int m0 = (tl % gx) * GBM, n0 = (tl / gx) * GBN;
     const int tap = n0 / Cin, ci0 = n0 - tap * Cin;
     const int ky = tap / 3, sdy = ky - 1, sdx = tap - ky * 3 - 1;
+    const int ti = tap >> 1, tj = tap & 1;            // CT: the sub-pixel of the output gradient
     const int ktiles = K / 16;
     const int kt0 = bz * kt_per_split;
     const int kt1 = min(ktiles, kt0 + kt_per_split);
@@ -1727,10 +1735,15 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
                 const int kk = kq + 8 * i;
                 const long long pix = (long long)(pn * H + ph) * W + pw + kk;
                 ra[ks][i] = ok ? ld4(dy + pix * lddy + m0 + c4) : f4zero();
-                const int hh = ph + sdy, ww = pw + kk + sdx;
-                rb[ks][i] = (ok && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
-                                ? ld4(x + ((long long)(pn * H + hh) * W + ww) * ldx + ci0 + c4)
-                                : f4zero();
+                if constexpr (CT) {
+                    const long long opix = (long long)(pn * 2 * H + 2 * ph + ti) * (2 * W) + 2 * (pw + kk) + tj;
+                    rb[ks][i] = ok ? ld4(x + opix * ldx + ci0 + c4) : f4zero();
+                } else {
+                    const int hh = ph + sdy, ww = pw + kk + sdx;
+                    rb[ks][i] = (ok && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                                    ? ld4(x + ((long long)(pn * H + hh) * W + ww) * ldx + ci0 + c4)
+                                    : f4zero();
+                }
             }
             pw += 16;
             if (pw >= W) { pw = 0; if (++ph == H) { ph = 0; ++pn; } }

@@ -374,6 +374,21 @@ CDM_API int cdm_convT2x2_wgrad_x16(const float* x, int N, int H, int W, int Cin,
     const int M = Cin, NN = 4 * Cout, K = N * H * W;
     const int sp = effective_splits(K, splits);
     EpiStore ep{slab, NN, (long long)M * NN, nullptr, 1, 0, nullptr, 0, M, NN};
+    static const bool tr = [] { const char* e = getenv("CDM_CONVT_WGRAD_TR"); return !e || atoi(e) != 0; }();
+    if (tr && Cin % 128 == 0 && Cout % 128 == 0 && W % 16 == 0 && ldx % 4 == 0 && lddy % 4 == 0 &&
+        effective_splits(K, splits, 16) == sp) {
+        // the transposed-read staging of the 3x3 weight gradient with the ConvT sub-pixel map ($CDM_CONVT_WGRAD_TR=0:
+        // the generic GEMM below)
+        const int ktiles = K / 16, per = (ktiles + sp - 1) / sp;
+        dim3 grid((M / GBM) * (NN / GBN) * ((ktiles + per - 1) / per));
+        if (nterm == NT_H3)
+            hipLaunchKernelGGL((wgrad3x3_tr_x3_kernel<NT_H3, 1, true>), grid, dim3(GTHREADS), 0, S(stream), x, ldx, Cin,
+                               dy, H, W, Cout, lddy, K, per, amax_x, amax_dy, ep);
+        else
+            hipLaunchKernelGGL((wgrad3x3_tr_x3_kernel<1, 1, true>), grid, dim3(GTHREADS), 0, S(stream), x, ldx, Cin, dy, H,
+                               W, Cout, lddy, K, per, amax_x, amax_dy, ep);
+        return cdm_status();
+    }
     return launch_gemm_x3<ColK<LdDenseAT>::template T, ColK<LdConvT2x2GatherB>::template T, EpiStore, false>(
         MkColK<LdDenseAT>{LdDenseAT{x, ldx, M, K}, amax_x},
         MkColK<LdConvT2x2GatherB>{LdConvT2x2GatherB{dy, H, W, Cout, lddy, K, NN}, amax_dy}, ep, M, NN, K, sp, nterm,

@@ -106,7 +106,7 @@ def test_conv3x3_channel_slices(L):
     assert out[..., :Cout].abs().max().item() == 0.0
 
 
-@pytest.mark.parametrize("N,Hin,Cin,Cout", [(2, 8, 64, 32), (1, 16, 512, 128), (3, 4, 16, 8)])
+@pytest.mark.parametrize("N,Hin,Cin,Cout", [(2, 8, 64, 32), (1, 16, 512, 128), (3, 4, 16, 8), (2, 32, 256, 128)])
 def test_convT2x2(L, N, Hin, Cin, Cout):
     torch.manual_seed(2)
     x = torch.randn(N, Cin, Hin, Hin); W = torch.randn(Cin, Cout, 2, 2) * 0.1; b = torch.randn(Cout)
