@@ -68,48 +68,7 @@ def _forward_pair(nf, H, B, math, seed=3):
     return out
 
 
-class _RoundBF16(torch.autograd.Function):
-    """A tensor stored in bf16 and its gradient stored in bf16 (torch.autocast's conv outputs)."""
-
-    @staticmethod
-    def forward(ctx, v):
-        return v.to(torch.bfloat16).to(v.dtype)
-
-    @staticmethod
-    def backward(ctx, g):
-        return g.to(torch.bfloat16).to(g.dtype)
-
-
-class _bf16_operands:
-    """Oracle hook: round the operands of every 3x3 conv with C_in > 1 and of the two ConvTranspose2d(k=2, s=2) to bf16
-    (fp32 accumulate), as C4 does (the C_in = 1 / C_out = 1 convs and up0 stay fp32 on both sides).  outputs=True also
-    stores those 3x3 convs' outputs and their gradients in bf16, as torch.autocast does (the HIP C4 train step stores
-    the fused chain's y and g in bf16, a subset of these, so this reference is the less precise one)."""
-
-    def __init__(self, outputs: bool = False):
-        self.outputs = outputs
-
-    def __enter__(self):
-        self.orig, self.orig_t = R.F.conv2d, R.F.conv_transpose2d
-
-        def bf(v):
-            return v.to(torch.bfloat16).to(v.dtype)
-
-        def conv(x, w, b=None, *a, **k):
-            if w.shape[-1] == 3 and w.shape[1] > 1:
-                out = self.orig(bf(x), bf(w), b, *a, **k)
-                return _RoundBF16.apply(out) if self.outputs else out
-            return self.orig(x, w, b, *a, **k)
-
-        def convt(x, w, b=None, *a, **k):
-            if w.shape[-1] == 2:
-                x, w = bf(x), bf(w)
-            return self.orig_t(x, w, b, *a, **k)
-        R.F.conv2d, R.F.conv_transpose2d = conv, convt
-        return self
-
-    def __exit__(self, *exc):
-        R.F.conv2d, R.F.conv_transpose2d = self.orig, self.orig_t
+from _bf16emu import _RoundBF16, _bf16_operands  # noqa: E402,F401  (shared with tests/golden/make_golden_r5_c4.py)
 
 
 def _grad_errors(nf, H, B, math, seed=4, emulate_bf16=False):
@@ -293,6 +252,40 @@ def test_c4_bf16_cfg_T1500_vs_emulated_oracle(w):
     _parity.record("c4_bf16_sample_T1500", w=w, rms_err=rh, rms_err_emulated=re_, final_err=float(eh[0]),
                    final_err_emulated=float(ee[0]))
     print(f"T=1500 bf16 w={w:g}: RMS deviation from fp64 HIP {rh:.3e}, emulated reference {re_:.3e}; final "
+          f"{eh[0]:.3e} / {ee[0]:.3e}")
+    assert rh <= max(1.5 * re_, 1e-3)
+
+
+def test_c4_bf16_nf128_T1500_vs_emulated_reference():
+    """C4's benchmarked trajectory: bf16 sampling at n_feat = 128, T = 1500, w = 0 (the golden of
+    test_sample_nf128_T1500_matches_reference: seeded init, n = 2, the golden's schedule, b_t.sqrt() table and CPU-RNG
+    draws).  Bar: the deviation from the golden's fp64 re-run, RMS over the final x and the 13 stored snapshots (each
+    relative to its max|x|), within 1.5x that of the reference's own sampler under C4's bf16 operand rounding (the CPU
+    oracle under _bf16_operands, same draws, precomputed by tests/golden/make_golden_r5_c4.py), at least 1e-3."""
+    import cdm_amd
+    g = np.load(os.path.join(GOLD, "sampler_T1500_nf128.npz"))
+    e = np.load(os.path.join(GOLD, "sampler_T1500_nf128_bf16emu.npz"))
+    T, nf = int(g["T"]), int(g["n_feat"])
+    torch.manual_seed(int(g["init_seed"]))
+    m = cdm_amd.ContextUnet(1, nf, 6, 64, conv_math="bf16").cuda().eval()
+    d = cdm_amd.DDPM(m, T, "cuda", z_source="host", sched_tensors=_parity.golden_schedule(T),
+                     sched_sb=_parity.golden_sqrt_b(T))
+    torch.manual_seed(int(g["w0_seed"]))
+    x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(g["params"]), 0.0)
+    keep = [int(s) for s in g["snap_keep"]]
+
+    def errs(final, snaps):
+        out = [float(np.abs(np.asarray(final, np.float64) - g["w0_x_fp64"]).max() / np.abs(g["w0_x_fp64"]).max())]
+        for j in range(len(keep)):
+            r = g["w0_inter_fp64"][j]
+            out.append(float(np.abs(np.asarray(snaps[j], np.float64) - r).max() / np.abs(r).max()))
+        return np.array(out)
+    eh = errs(x.cpu().numpy(), [inter[s] for s in keep])
+    ee = errs(e["w0_x_bf16emu"], e["w0_inter_bf16emu"])
+    rh, re_ = float(np.sqrt((eh ** 2).mean())), float(np.sqrt((ee ** 2).mean()))
+    _parity.record("c4_bf16_sample_nf128_T1500", w=0.0, rms_err=rh, rms_err_emulated=re_, final_err=float(eh[0]),
+                   final_err_emulated=float(ee[0]))
+    print(f"C4 nf128 T=1500: RMS deviation from fp64 HIP {rh:.3e}, emulated reference {re_:.3e}; final "
           f"{eh[0]:.3e} / {ee[0]:.3e}")
     assert rh <= max(1.5 * re_, 1e-3)
 
