@@ -47,15 +47,23 @@ def _shortcut(C):
     return R.draw_shortcut(C, NF)
 
 
+@pytest.mark.parametrize("train", [True, False])
 @pytest.mark.parametrize("C", [2, 3, 16])
 @pytest.mark.parametrize("math", ["fp32", "h3"])
-def test_in_channels_train_grads(C, math):
+def test_in_channels_train_grads(C, math, train):
+    """train=False: gradients through model.eval() (BatchNorm frozen on running statistics made non-trivial by one
+    train forward first; they must not move)"""
     import cdm_amd
     from _kinks import Kinks, hip_kinks
     torch.manual_seed(5 + C)
     m = cdm_amd.ContextUnet(C, NF, NCF, H, conv_math=math).cuda().train()
-    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     g = torch.Generator().manual_seed(40 + C)
+    if not train:
+        with torch.no_grad():
+            m(torch.randn(B, C, H, H, generator=g).cuda(), torch.rand(B, generator=g).cuda(),
+              torch.rand(B, NCF, generator=g).cuda())
+        m.eval()
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     x = torch.randn(B, C, H, H, generator=g)
     t = torch.rand(B, generator=g)
     c = torch.rand(B, NCF, generator=g)
@@ -65,15 +73,18 @@ def test_in_channels_train_grads(C, math):
     eps = m(xg, tg, cg)
     assert eps.shape == (B, C, H, H)
     (eps * weight.cuda()).sum().backward()
+    if not train:
+        for k, v in m.state_dict().items():
+            assert torch.equal(v.cpu(), sd[k]), k
     torch.manual_seed(9)
     sc = _shortcut(C)
     hip = {"x": xg.grad, "t": tg.grad, "c": cg.grad, **{k: p.grad for k, p in m.named_parameters()}}
     m.load_state_dict(sd)
-    hk_relu, hk_pool = hip_kinks(m, x, t, c, sc, frozen=False)
-    e64h, g64h = _oracle(C, sd, x, t, c, sc, torch.float64, weight, True, Kinks(hk_relu, hk_pool))
+    hk_relu, hk_pool = hip_kinks(m, x, t, c, sc, frozen=not train)
+    e64h, g64h = _oracle(C, sd, x, t, c, sc, torch.float64, weight, train, Kinks(hk_relu, hk_pool))
     cap32 = Kinks()
-    e32, g32 = _oracle(C, sd, x, t, c, sc, torch.float32, weight, True, cap32)
-    e64r, g64r = _oracle(C, sd, x, t, c, sc, torch.float64, weight, True, Kinks(cap32.relu, cap32.pool))
+    e32, g32 = _oracle(C, sd, x, t, c, sc, torch.float32, weight, train, cap32)
+    e64r, g64r = _oracle(C, sd, x, t, c, sc, torch.float64, weight, train, Kinks(cap32.relu, cap32.pool))
     bad = []
     e_h, e_r = _rel(eps.detach(), e64h), _rel(e32, e64r)
     if e_h > 3 * e_r + 2e-6:
@@ -82,7 +93,7 @@ def test_in_channels_train_grads(C, math):
     for k, ref in g64h.items():
         got = hip[k]
         assert got is not None and tuple(got.shape) == tuple(ref.shape), k
-        if ".conv1.0.bias" in k or ".conv2.0.bias" in k:       # BN-fed conv bias: analytic gradient 0
+        if train and (".conv1.0.bias" in k or ".conv2.0.bias" in k):   # BN-fed conv bias: analytic gradient 0 (batch BN)
             if got.abs().max().item() > 1e-4 * gmax:
                 bad.append((k, got.abs().max().item(), 0.0))
             continue
