@@ -571,9 +571,22 @@ __global__ __launch_bounds__(256) void bn_bwd_dy_kernel(const GT* __restrict__ g
                                                         OT* __restrict__ dy, int lddy) {
     const int C8 = C >> 3;
     const long long total = P * C8;
-    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (long long)gridDim.x * blockDim.x) {
-        const int c8 = (int)(idx % C8) * 8;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    // the grid stride is a multiple of C8 (host: C8 divides 256), so a thread keeps its channel octet: its 72
+    // coefficients are loaded once, not per element (the per-element scalar loads held the pass at 3.8 TB/s)
+    const long long idx0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int c8 = (int)(idx0 % C8) * 8;
+    float cf[7][8];
+    {
+        const float* src[7] = {s, t, mean, invstd, A, B, Cc};
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const float4 a = ld4(src[k] + c8), b = ld4(src[k] + c8 + 4);
+            cf[k][0] = a.x; cf[k][1] = a.y; cf[k][2] = a.z; cf[k][3] = a.w;
+            cf[k][4] = b.x; cf[k][5] = b.y; cf[k][6] = b.z; cf[k][7] = b.w;
+        }
+    }
+    for (long long idx = idx0; idx < total; idx += stride) {
         const long long pix = idx / C8;
         const float4 g0 = Act<GT>::to4(Act<GT>::load4(g + pix * ldg + c8));
         const float4 g1 = Act<GT>::to4(Act<GT>::load4(g + pix * ldg + c8 + 4));
@@ -582,9 +595,8 @@ __global__ __launch_bounds__(256) void bn_bwd_dy_kernel(const GT* __restrict__ g
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int c = c8 + j;
             const float gv = j < 4 ? f4get(g0, j) : f4get(g1, j - 4), yv = j < 4 ? f4get(y0, j) : f4get(y1, j - 4);
-            o[j] = bn_bwd_elem(gv, yv, s[c], t[c], mean[c], invstd[c], A[c], B[c], Cc[c]);
+            o[j] = bn_bwd_elem(gv, yv, cf[0][j], cf[1][j], cf[2][j], cf[3][j], cf[4][j], cf[5][j], cf[6][j]);
         }
         OT* d = dy + pix * lddy + c8;
         if constexpr (std::is_same<OT, float>::value) {
@@ -889,7 +901,7 @@ CDM_API int cdm_bn_bwd_dy(const void* g, int ldg, const void* y, int ldy, long l
                           const float* t, const float* mean, const float* invstd, const float* A, const float* B,
                           const float* Cc, void* dy, int lddy, int dt, void* stream) {
     // dt bit 0: g and y are bf16, bit 1: dy is stored as bf16
-    if (C % 8 || ldg % 8 || ldy % 8 || lddy % 8 || P < 0) return (int)hipErrorInvalidValue;
+    if (C % 8 || 256 % (C / 8) || ldg % 8 || ldy % 8 || lddy % 8 || P < 0) return (int)hipErrorInvalidValue;
     if (P == 0) return 0;
     const int nb = ew_blocks(P * (C / 8));
     auto run = [&](auto gtag, auto otag) {

@@ -157,11 +157,11 @@ class UNetEngine:
         # $CDM_ACT16=0 keeps fp32 activations (A/B checks).
         self.act16 = self.nterm == 1 and os.environ.get("CDM_ACT16", "1") != "0"
         # bf16 (one-term) arithmetic: dy of a fused layer by a separate elementwise pass (cdm_bn_bwd_dy) and the
-        # dgrad on the plain staging schedule instead of the BN-backward staging ($CDM_DY_PASS=1; off: same-box A/B,
-        # 2 runs each, C4 28.20 -> 28.31-28.33 ms per step — the pass costs 213 us per 64^2 layer, more than the dgrad
-        # gains, profiles/r4_ab_sums_dy_pass.txt; the 36.7 -> 34.7 ms of profiles/r4_ab_dy_pass_gn_out.txt was measured
-        # on a build whose conv epilogue spilled)
-        self.dy_pass = self.dy_store and self.nterm == 1 and os.environ.get("CDM_DY_PASS", "0") == "1"
+        # dgrad on the forward's staging schedule (halo two chunks ahead) instead of the BN-backward staging.  Round 4
+        # kept it off (C4 28.20 -> 28.31-28.33 ms: the pass took 213 us per 64^2 layer, profiles/r4_ab_sums_dy_pass.txt);
+        # round 5 loads the pass's per-channel coefficients once per thread instead of per element, and it pays: same-box
+        # A/B, 2 runs each, C4 27.33-27.38 -> 26.86-26.89 ms per step (profiles/r5_ab_dy_pass.txt).  $CDM_DY_PASS=0: off
+        self.dy_pass = self.dy_store and self.nterm == 1 and os.environ.get("CDM_DY_PASS", "1") == "1"
         # train: out.1's GroupNorm + ReLU inside out.3's forward and weight-gradient staging, zO never written
         # ($CDM_FUSE_GN_OUT=0: the apply kernel writes zO)
         self.fuse_gn_out = os.environ.get("CDM_FUSE_GN_OUT", "1") != "0"
