@@ -1,6 +1,6 @@
 """Round-5 fixture for the C4 (bf16) benchmarked trajectory (build container; CPU only, no reference import).
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_r5_c4.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_r5_c4.py [w]     (w = 0: the default; 3: the CFG golden)
 
 sampler_T1500_nf128_bf16emu.npz — the trajectory of tests/golden/sampler_T1500_nf128.npz (n_feat = 128 seeded default
 init, n = 2, w = 0, T = 1500, the golden's schedule, CPU-RNG replay with the golden's seed) re-run by the CPU oracle
@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 
 
-def main():
+def main(w: float = 0.0):
     import numpy as np
     import torch
     import cdm_amd
@@ -31,23 +31,25 @@ def main():
     from oracle import ref_cpu as R
 
     torch.set_num_threads(int(os.environ.get("CDM_GOLDEN_THREADS", "8")))
-    g = np.load(os.path.join(HERE, "sampler_T1500_nf128.npz"))
+    g = np.load(os.path.join(HERE, "sampler_T1500_nf128.npz" if w == 0 else f"sampler_T1500_nf128_w{w:g}.npz"))
     T, nf = int(g["T"]), int(g["n_feat"])
     torch.manual_seed(int(g["init_seed"]))
     sd = {k: v.detach().clone() for k, v in cdm_amd.ContextUnet(1, nf, 6, 64).state_dict().items()}
     t0 = time.time()
     with _bf16_operands():
-        torch.manual_seed(int(g["w0_seed"]))
+        torch.manual_seed(int(g[f"w{w:g}_seed"]))
         x, inter = R.sample_ddpm(R.make_model_fn(R.clone_sd(sd), n_feat=nf, n_cfeat=6, height=64), 2, 64,
-                                 torch.from_numpy(g["params"]), 0.0, T, _parity.golden_schedule(T), 6)
+                                 torch.from_numpy(g["params"]), w, T, _parity.golden_schedule(T), 6)
     keep = [int(s) for s in g["snap_keep"]]
-    out = {"w0_x_bf16emu": x.numpy(), "w0_inter_bf16emu": inter.numpy()[keep], "snap_keep": g["snap_keep"],
+    k = f"w{w:g}"
+    out = {f"{k}_x_bf16emu": x.numpy(), f"{k}_inter_bf16emu": inter.numpy()[keep], "snap_keep": g["snap_keep"],
            "T": g["T"], "n_feat": g["n_feat"]}
-    ref = g["w0_x_fp64"]
-    print(f"emulated bf16 run {time.time() - t0:.0f} s; final deviation from fp64 "
-          f"{np.abs(out['w0_x_bf16emu'] - ref).max() / np.abs(ref).max():.3e}")
-    np.savez_compressed(os.path.join(HERE, "sampler_T1500_nf128_bf16emu.npz"), **out)
+    ref = g[f"{k}_x_fp64"]
+    print(f"w={w:g}: emulated bf16 run {time.time() - t0:.0f} s; final deviation from fp64 "
+          f"{np.abs(out[f'{k}_x_bf16emu'] - ref).max() / np.abs(ref).max():.3e}")
+    name = "sampler_T1500_nf128_bf16emu.npz" if w == 0 else f"sampler_T1500_nf128_w{w:g}_bf16emu.npz"
+    np.savez_compressed(os.path.join(HERE, name), **out)
 
 
 if __name__ == "__main__":
-    main()
+    main(float(sys.argv[1]) if len(sys.argv) > 1 else 0.0)

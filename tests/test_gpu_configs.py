@@ -256,36 +256,38 @@ def test_c4_bf16_cfg_T1500_vs_emulated_oracle(w):
     assert rh <= max(1.5 * re_, 1e-3)
 
 
-def test_c4_bf16_nf128_T1500_vs_emulated_reference():
-    """C4's benchmarked trajectory: bf16 sampling at n_feat = 128, T = 1500, w = 0 (the golden of
+@pytest.mark.parametrize("w", [0.0, 3.0])
+def test_c4_bf16_nf128_T1500_vs_emulated_reference(w):
+    """C4's benchmarked trajectories: bf16 sampling at n_feat = 128, T = 1500, w = 0 and the CFG w = 3 (the goldens of
     test_sample_nf128_T1500_matches_reference: seeded init, n = 2, the golden's schedule, b_t.sqrt() table and CPU-RNG
     draws).  Bar: the deviation from the golden's fp64 re-run, RMS over the final x and the 13 stored snapshots (each
     relative to its max|x|), within 1.5x that of the reference's own sampler under C4's bf16 operand rounding (the CPU
     oracle under _bf16_operands, same draws, precomputed by tests/golden/make_golden_r5_c4.py), at least 1e-3."""
     import cdm_amd
-    g = np.load(os.path.join(GOLD, "sampler_T1500_nf128.npz"))
-    e = np.load(os.path.join(GOLD, "sampler_T1500_nf128_bf16emu.npz"))
+    k = f"w{w:g}"
+    g = np.load(os.path.join(GOLD, "sampler_T1500_nf128.npz" if w == 0 else f"sampler_T1500_nf128_{k}.npz"))
+    e = np.load(os.path.join(GOLD, "sampler_T1500_nf128_bf16emu.npz" if w == 0 else f"sampler_T1500_nf128_{k}_bf16emu.npz"))
     T, nf = int(g["T"]), int(g["n_feat"])
     torch.manual_seed(int(g["init_seed"]))
     m = cdm_amd.ContextUnet(1, nf, 6, 64, conv_math="bf16").cuda().eval()
     d = cdm_amd.DDPM(m, T, "cuda", z_source="host", sched_tensors=_parity.golden_schedule(T),
                      sched_sb=_parity.golden_sqrt_b(T))
-    torch.manual_seed(int(g["w0_seed"]))
-    x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(g["params"]), 0.0)
+    torch.manual_seed(int(g[f"{k}_seed"]))
+    x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(g["params"]), w)
     keep = [int(s) for s in g["snap_keep"]]
 
     def errs(final, snaps):
-        out = [float(np.abs(np.asarray(final, np.float64) - g["w0_x_fp64"]).max() / np.abs(g["w0_x_fp64"]).max())]
+        out = [float(np.abs(np.asarray(final, np.float64) - g[f"{k}_x_fp64"]).max() / np.abs(g[f"{k}_x_fp64"]).max())]
         for j in range(len(keep)):
-            r = g["w0_inter_fp64"][j]
+            r = g[f"{k}_inter_fp64"][j]
             out.append(float(np.abs(np.asarray(snaps[j], np.float64) - r).max() / np.abs(r).max()))
         return np.array(out)
     eh = errs(x.cpu().numpy(), [inter[s] for s in keep])
-    ee = errs(e["w0_x_bf16emu"], e["w0_inter_bf16emu"])
+    ee = errs(e[f"{k}_x_bf16emu"], e[f"{k}_inter_bf16emu"])
     rh, re_ = float(np.sqrt((eh ** 2).mean())), float(np.sqrt((ee ** 2).mean()))
-    _parity.record("c4_bf16_sample_nf128_T1500", w=0.0, rms_err=rh, rms_err_emulated=re_, final_err=float(eh[0]),
+    _parity.record("c4_bf16_sample_nf128_T1500", w=w, rms_err=rh, rms_err_emulated=re_, final_err=float(eh[0]),
                    final_err_emulated=float(ee[0]))
-    print(f"C4 nf128 T=1500: RMS deviation from fp64 HIP {rh:.3e}, emulated reference {re_:.3e}; final "
+    print(f"C4 nf128 T=1500 w={w:g}: RMS deviation from fp64 HIP {rh:.3e}, emulated reference {re_:.3e}; final "
           f"{eh[0]:.3e} / {ee[0]:.3e}")
     assert rh <= max(1.5 * re_, 1e-3)
 

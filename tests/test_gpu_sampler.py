@@ -259,21 +259,23 @@ def test_sample_nf128_matches_reference(w):
     _trajectory_check("sample_nf128_T400", sfx, x.cpu().numpy(), inter, w, conv_math=m.conv_math)
 
 
-def test_sample_nf128_T1500_matches_reference():
-    """The benchmarked trajectory: sample_ddpm (code/train_diffusion_condition.py:281-335) at n_feat = 128, T = 1500,
-    w = 0 (seeded default init), n = 2, CPU-RNG replay, vs the reference's run and its fp64 re-run
-    (tests/golden/make_golden_r5.py).  Bar: _trajectory_check (1.5x the golden's own fp32 deviation, no floor)."""
+@pytest.mark.parametrize("w", [0.0, 3.0])
+def test_sample_nf128_T1500_matches_reference(w):
+    """The benchmarked trajectories: sample_ddpm (code/train_diffusion_condition.py:281-335) at n_feat = 128, T = 1500,
+    w = 0 and the CFG w = 3 (seeded default init), n = 2, CPU-RNG replay, vs the reference's runs and their fp64 re-runs
+    (tests/golden/make_golden_r5.py, make_golden_r5_w3.py).  Bar: _trajectory_check (1.5x the golden's own fp32
+    deviation, no floor)."""
     import cdm_amd
-    path = os.path.join(GOLD, "sampler_T1500_nf128.npz")
+    path = os.path.join(GOLD, "sampler_T1500_nf128.npz" if w == 0 else "sampler_T1500_nf128_w3.npz")
     sfx = np.load(path)
     T, nf = int(sfx["T"]), int(sfx["n_feat"])
     torch.manual_seed(int(sfx["init_seed"]))
     m = cdm_amd.ContextUnet(1, nf, 6, 64).cuda().eval()
     d = _golden_ddpm(m, T)
-    torch.manual_seed(int(sfx["w0_seed"]))
-    x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(sfx["params"]), 0.0)
+    torch.manual_seed(int(sfx[f"w{w:g}_seed"]))
+    x, inter = d.sample_ddpm(2, 64, None, torch.from_numpy(sfx["params"]), w)
     assert inter.shape[0] == 82
-    _trajectory_check("sample_nf128_T1500", sfx, x.cpu().numpy(), inter, 0.0, conv_math=m.conv_math)
+    _trajectory_check("sample_nf128_T1500", sfx, x.cpu().numpy(), inter, w, conv_math=m.conv_math)
 
 
 def test_device_z_fresh_per_call_and_seedable():
