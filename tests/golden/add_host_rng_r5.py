@@ -18,8 +18,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 from oracle import ref_cpu as R  # noqa: E402
 
-# (fixture key, seed, n_feat, T): sampler_T1500_nf8.npz (w = 0) and sampler_T1500_nf128.npz
-SEQUENCES = (("seq_T1500_nf8_w0", 700, 8, 1500), ("seq_T1500_nf128_w0", 900, 128, 1500))
+# (fixture key, seed, n_feat, T): sampler_T1500_nf8.npz (w = 0), sampler_T1500_nf128.npz and sampler_T1500_nf128_w3.npz
+# (CFG: one forward of the 2n batch per step, so the same draw order — x_T, then per step z and one shortcut)
+SEQUENCES = (("seq_T1500_nf8_w0", 700, 8, 1500), ("seq_T1500_nf128_w0", 900, 128, 1500),
+             ("seq_T1500_nf128_w3", 901, 128, 1500))
 
 
 def sequence_hash(seed: int, nf: int, T: int, n: int = 2) -> str:
