@@ -280,7 +280,8 @@ def cpu_baseline(threads: int):
     dt1, sd1 = _cpu_train_rate(R, 64, T1, 8, steps=5, warmup=1)
     s01 = _cpu_sample_rate(R, sd1, 64, T1, 8, 0.0, 10)
     return {
-        "value": bs / dt, "unit": "images/s", "cores": cores, "threads": threads, "affinity_cpus": aff,
+        "value": bs / dt, "unit": "images/s", "cores": threads, "threads": threads, "host_cpus": cores,
+        "affinity_cpus": aff,
         "cgroup_cpu_quota": quota, "kind": "port",
         "sample": f"C2 shape: 1 train step (perturb + fwd + mse + bwd + Adam) at bs={bs}, n_feat=128, 64x64, timed "
                   f"directly after a bs=8 warm-up step; CPU oracle = torch CPU fp32 restatement of the reference path on "
