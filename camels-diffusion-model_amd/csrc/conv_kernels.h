@@ -268,11 +268,29 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
                 }
             }
         } else {
+            // every coefficient and shortcut input loaded ahead of the first store: y may alias them as far as the
+            // compiler knows, so a load written next to its use waits behind the previous store (RESID cost the
+            // 64^2 init conv 300 us per launch that way)
             const int sel = img >= fz.split ? N : 0;
+            const bool resid = fz.kind == FUSE_RESID;
+            float ca[2], cb[2], xv[2][16];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int n = nw + 32 * j + (lane & 31);
+                ca[j] = resid ? fz.w[sel + n] : fz.fa[img * fz.fan + n];
+                cb[j] = resid ? fz.b[sel + n] : fz.fb[img * fz.fbn + n];
+            }
+            if (resid) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        xv[i][r] = fz.x[mw + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
+            }
             CDM_FOR_ACC({
                 float v = relu_f(acc[i][j][r] + bj[j]);
-                if (fz.kind == FUSE_RESID) v = fmaf(fz.w[sel + n], fz.x[m], fz.b[sel + n]) + v;
-                else v = fmaf(fz.fa[img * fz.fan + n], v, fz.fb[img * fz.fbn + n]);
+                if (resid) v = fmaf(ca[j], xv[i][r], cb[j]) + v;
+                else v = fmaf(ca[j], v, cb[j]);
                 v = Act<OT>::round(v);
                 Act<OT>::store(y + (long long)m * ldy + n, v);
                 am = fmaxf(am, fabsf(v));
