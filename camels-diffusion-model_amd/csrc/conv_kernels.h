@@ -1039,6 +1039,122 @@ __global__ __launch_bounds__(GTHREADS, MINB) void gemm_x3_kernel(SA sa0, SB sb0,
     e(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
 }
 
+// Dense-A x pre-split-B GEMM with a two-deep register prefetch (the ConvT 2x2 forward: K = Cin = 256 / 512, so a
+// block's whole life is 16-32 K tiles, and gemm_x3's one-deep prefetch left every tile waiting on the HBM latency of
+// the A loads issued one tile earlier — 12 MFMAs per wave per tile cannot cover it).  Tiles kt + 1 and kt + 2 are
+// in flight while tile kt computes: two register sets, the loop unrolled by two so each set has a fixed role.
+// Same block tile, LDS images, fragment order and MFMA order per K tile as gemm_x3_kernel<StageRowK<LdDenseA>,
+// StagePre> (bit-identical results); every load unconditional (M % 128 == 0, N % 128 == 0, K % 32 == 0: the
+// host checks), the last tiles re-load tile nk - 1 instead of branching.
+template <int NT, class EP, int MINB>
+__global__ __launch_bounds__(GTHREADS, MINB) void gemm_deep_kernel(const float* __restrict__ a, long long lda,
+                                                                  const __bf16* __restrict__ bp, int N,
+                                                                  const float* amax_a, const float* amax_b, EP ep,
+                                                                  int K) {
+    constexpr int NS = XTerms<NT>::NS;
+    constexpr int TILE = NS * XPLANE;
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TILE];
+    __bf16* As = smem;                 // [buf][term][row][16 k] (xoff swizzle)
+    __bf16* Bs = smem + 2 * TILE;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // operand-sharing order (gemm_x3 order 1): XCD-contiguous flat ids, column tile fastest
+    const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy;
+    int bx, by;
+    {
+        const int L = blockIdx.x + gx * blockIdx.y, q = nwg >> 3, r = nwg & 7, xcd = L & 7, j = L >> 3;
+        const int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+        by = l % gy; bx = l / gy;
+    }
+    const int m0 = bx * GBM, n0 = by * GBN, nk = K / XBK;
+    const float sa = op_scale<NT>(amax_a), sb = op_scale<NT>(amax_b);
+    const float* arow[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) arow[i] = a + (long long)(m0 + tid / 4 + i * (GTHREADS / 4)) * lda + (tid % 4) * 4;
+    const __bf16* brow = bp + (long long)(n0 + (tid >> 1)) * XBK + (tid & 1) * 8;
+    const long long bstride = (long long)N * XBK;   // one term plane of a K tile ([ktiles][3][N][16])
+    struct Regs { float4 a[2]; u32x4 b[NS]; };
+    auto gload = [&](Regs& R, int kt) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) R.a[i] = ld4(arow[i] + kt * XBK);
+#pragma unroll
+        for (int t = 0; t < NS; ++t) R.b[t] = *reinterpret_cast<const u32x4*>(brow + ((long long)kt * 3 + t) * bstride);
+    };
+    auto sstore = [&](const Regs& R, int buf) {
+        __bf16* ab = As + buf * TILE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float x[4] = {R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w};
+            __bf16 h[4], m[4], l[4];
+            split_terms<NT>(x, sa, h, m, l);
+            __bf16* d = ab + xoff(tid / 4 + i * (GTHREADS / 4), (tid % 4) * 4);
+            *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
+            if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + XPLANE) = bf16x4{m[0], m[1], m[2], m[3]};
+            if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + 2 * XPLANE) = bf16x4{l[0], l[1], l[2], l[3]};
+        }
+        __bf16* d = Bs + buf * TILE + xoff(tid >> 1, (tid & 1) * 8);
+#pragma unroll
+        for (int t = 0; t < NS; ++t) *reinterpret_cast<u32x4*>(d + t * XPLANE) = R.b[t];
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31), kh = (lane >> 5) * 8;
+    int aoff[2], boff[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) { aoff[i] = xoff(ar + 32 * i, kh); boff[i] = xoff(br + 32 * i, kh); }
+    auto mm = [&](int buf) {
+        const __bf16* ab = As + buf * TILE;
+        const __bf16* bb = Bs + buf * TILE;
+        bf16x8 fa[2][NS], fb[2][NS];
+#pragma unroll
+        for (int t = 0; t < NS; ++t)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                fa[i][t] = *reinterpret_cast<const bf16x8*>(ab + t * XPLANE + aoff[i]);
+                fb[i][t] = *reinterpret_cast<const bf16x8*>(bb + t * XPLANE + boff[i]);
+            }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x16 c = acc[i][j];
+                if constexpr (NT >= 6) {
+                    c = xmfma<NT>(fa[i][1], fb[j][1], c);
+                    c = xmfma<NT>(fa[i][2], fb[j][0], c);
+                    c = xmfma<NT>(fa[i][0], fb[j][2], c);
+                }
+                if constexpr (NT >= 3) {
+                    c = xmfma<NT>(fa[i][1], fb[j][0], c);
+                    c = xmfma<NT>(fa[i][0], fb[j][1], c);
+                }
+                acc[i][j] = xmfma<NT>(fa[i][0], fb[j][0], c);
+            }
+    };
+    Regs R0, R1;
+    gload(R0, 0);
+    gload(R1, 1);
+    sstore(R0, 0);
+    __syncthreads();
+    // top of an iteration: LDS buffer 0 holds tile kt, R1 tile kt + 1 (in flight)
+    for (int kt = 0; kt < nk; kt += 2) {
+        gload(R0, min(kt + 2, nk - 1));
+        mm(0);
+        sstore(R1, 1);
+        __syncthreads();
+        gload(R1, min(kt + 3, nk - 1));
+        mm(1);
+        if (kt + 2 < nk) sstore(R0, 0);
+        __syncthreads();
+    }
+    unscale<NT>(acc, sa, sb);
+    ep(acc, m0 + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(smem), tid);
+}
+
 // $CDM_GEMM_MINB: 4 or 2 resident blocks per CU asked of the compiler; default 4 for h3 (profiles/r3_ab_gemm_minb.txt),
 // 2 for the one-term bf16 arithmetic, whose 4-block form spills 51 VGPRs (with the bf16 knobs below, same-box A/B:
 // C4 27.95-28.02 -> 27.73-27.75 ms per step, profiles/r4_ab_c4_knobs.txt)

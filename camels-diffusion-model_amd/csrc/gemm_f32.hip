@@ -326,6 +326,20 @@ CDM_API int cdm_convT2x2_fwd_x16(const float* x, int N, int H, int W, int Cin, i
     if (!x16_ok(nterm) || Cin % 4 || Cout % 4 || !x16_amax_ok(nterm, amax_x, amax_w)) return (int)hipErrorInvalidValue;
     const int M = N * H * W, K = Cin, NN = 4 * Cout;
     EpiConvT2x2 ep{y, ldy, bias, H, W, Cout, M, NN, amax_y};
+    // the two-deep prefetch form where the shape allows ($CDM_CONVT_DEEP=0: gemm_x3, read per call for A/B tests)
+    const char* dv = getenv("CDM_CONVT_DEEP");
+    if ((!dv || atoi(dv) != 0) && M % GBM == 0 && NN % GBN == 0 && K % (2 * XBK) == 0 && ldx % 4 == 0 &&
+        (nterm == NT_H3 || nterm == 1)) {
+        const dim3 grid(M / GBM, NN / GBN);
+        const __bf16* wb = reinterpret_cast<const __bf16*>(wx);
+        if (nterm == NT_H3)
+            hipLaunchKernelGGL((gemm_deep_kernel<NT_H3, EpiConvT2x2, 3>), grid, dim3(GTHREADS), 0, S(stream), x,
+                               (long long)ldx, wb, NN, amax_x, amax_w, ep, K);
+        else
+            hipLaunchKernelGGL((gemm_deep_kernel<1, EpiConvT2x2, 3>), grid, dim3(GTHREADS), 0, S(stream), x,
+                               (long long)ldx, wb, NN, amax_x, amax_w, ep, K);
+        return cdm_status();
+    }
     return launch_gemm_x3<RowK<LdDenseA>::template T, StagePre, EpiConvT2x2, true>(
         MkRowK<LdDenseA>{LdDenseA{x, ldx, M, K}, amax_x}, MkPre{reinterpret_cast<const __bf16*>(wx), NN, amax_w}, ep,
         M, NN, K, 1, nterm, S(stream));

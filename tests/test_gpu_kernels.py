@@ -135,6 +135,29 @@ def test_convT2x2(L, N, Hin, Cin, Cout):
     torch.cuda.synchronize()
     _close(_nchw(y3, N, 2 * Hin, 2 * Hin, Cout), ref.detach())
     assert am3.item() == y3.abs().max().item()
+    # the two-deep prefetch kernel (default where M, 4 Cout % 128 == 0 and Cin % 32 == 0) against gemm_x3: the same
+    # products in the same order, bit for bit — h3 and the one-term bf16 form
+    wxb = torch.empty((Cin + 15) // 16 * 3 * 4 * Cout * 16, dtype=torch.bfloat16, device="cuda")
+    L.cdm_split_bf16x3(wt.data_ptr(), 4 * Cout, Cin, 4 * Cout, wxb.data_ptr(), _s())
+    outs = {}
+    for deep in ("1", "0"):
+        os.environ["CDM_CONVT_DEEP"] = deep
+        try:
+            for nterm, w_, aw in ((4, wx, amw), (1, wxb, None)):
+                o = torch.empty_like(y); ao = torch.zeros(1, device="cuda")
+                L.cdm_convT2x2_fwd_x16(xn.data_ptr(), N, Hin, Hin, Cin, Cin, w_.data_ptr(),
+                                       amx.data_ptr() if aw is not None else None,
+                                       aw.data_ptr() if aw is not None else None, bc.data_ptr(), o.data_ptr(), Cout,
+                                       Cout, ao.data_ptr(), nterm, _s())
+                torch.cuda.synchronize()
+                outs[deep, nterm] = (o, ao)
+        finally:
+            del os.environ["CDM_CONVT_DEEP"]
+    for nterm in (4, 1):
+        assert torch.equal(outs["1", nterm][0], outs["0", nterm][0]) and torch.equal(outs["1", nterm][1],
+                                                                                     outs["0", nterm][1])
+    assert torch.equal(outs["1", 4][0], y3)
+    _close(_nchw(outs["1", 1][0], N, 2 * Hin, 2 * Hin, Cout), ref.detach(), 2e-2)
     gyn = _nhwc(gy)
     dx = torch.empty(N * Hin * Hin, Cin, device="cuda")
     L.cdm_convT2x2_dgrad(gyn.data_ptr(), N, Hin, Hin, Cout, Cout, wtT.data_ptr(), dx.data_ptr(), Cin, Cin, 0, _s())
