@@ -1046,9 +1046,25 @@ __global__ __launch_bounds__(GTHREADS, MINB) void gemm_x3_kernel(SA sa0, SB sb0,
 // Same block tile, LDS images, fragment order and MFMA order per K tile as gemm_x3_kernel<StageRowK<LdDenseA>,
 // StagePre> (bit-identical results); every load unconditional (M % 128 == 0, N % 128 == 0, K % 32 == 0: the
 // host checks), the last tiles re-load tile nk - 1 instead of branching.
-template <int NT, class EP, int MINB>
-__global__ __launch_bounds__(GTHREADS, MINB) void gemm_deep_kernel(const float* __restrict__ a, long long lda,
-                                                                  const __bf16* __restrict__ bp, int N,
+// AL: the A addresses — base(m) the row's origin, off(kt) the block-uniform element offset of K tile kt (16 k)
+struct DeepDenseA {          // A[m][k] = a[m lda + k]
+    const float* a; long long lda;
+    __device__ __forceinline__ const float* base(int m) const { return a + (long long)m * lda; }
+    __device__ __forceinline__ long long off(int kt) const { return (long long)kt * XBK; }
+};
+struct DeepConvT2x2GatherA { // the ConvT 2x2 input gradient (LdConvT2x2GatherA): m = (n, h, w), k = (i 2 + j) Co + co
+    const float* dy; int H, W, Co; long long lddy;
+    __device__ __forceinline__ const float* base(int m) const {
+        const int hw = H * W, n = m / hw, rem = m - n * hw, h = rem / W, w = rem - h * W;
+        return dy + ((long long)(n * 2 * H + 2 * h) * (2 * W) + 2 * w) * lddy;
+    }
+    __device__ __forceinline__ long long off(int kt) const {   // a 16-k tile lies in one sub-pixel (Co % 16 == 0)
+        const int k0 = kt * XBK, ij = k0 / Co, co = k0 - ij * Co;
+        return ((long long)(ij >> 1) * (2 * W) + (ij & 1)) * lddy + co;
+    }
+};
+template <int NT, class AL, class EP, int MINB>
+__global__ __launch_bounds__(GTHREADS, MINB) void gemm_deep_kernel(AL al, const __bf16* __restrict__ bp, int N,
                                                                   const float* amax_a, const float* amax_b, EP ep,
                                                                   int K) {
     constexpr int NS = XTerms<NT>::NS;
@@ -1070,13 +1086,14 @@ __global__ __launch_bounds__(GTHREADS, MINB) void gemm_deep_kernel(const float* 
     const float sa = op_scale<NT>(amax_a), sb = op_scale<NT>(amax_b);
     const float* arow[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) arow[i] = a + (long long)(m0 + tid / 4 + i * (GTHREADS / 4)) * lda + (tid % 4) * 4;
+    for (int i = 0; i < 2; ++i) arow[i] = al.base(m0 + tid / 4 + i * (GTHREADS / 4)) + (tid % 4) * 4;
     const __bf16* brow = bp + (long long)(n0 + (tid >> 1)) * XBK + (tid & 1) * 8;
     const long long bstride = (long long)N * XBK;   // one term plane of a K tile ([ktiles][3][N][16])
     struct Regs { float4 a[2]; u32x4 b[NS]; };
     auto gload = [&](Regs& R, int kt) {
+        const long long ko = al.off(kt);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) R.a[i] = ld4(arow[i] + kt * XBK);
+        for (int i = 0; i < 2; ++i) R.a[i] = ld4(arow[i] + ko);
 #pragma unroll
         for (int t = 0; t < NS; ++t) R.b[t] = *reinterpret_cast<const u32x4*>(brow + ((long long)kt * 3 + t) * bstride);
     };

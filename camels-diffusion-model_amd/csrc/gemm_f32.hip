@@ -333,11 +333,11 @@ CDM_API int cdm_convT2x2_fwd_x16(const float* x, int N, int H, int W, int Cin, i
         const dim3 grid(M / GBM, NN / GBN);
         const __bf16* wb = reinterpret_cast<const __bf16*>(wx);
         if (nterm == NT_H3)
-            hipLaunchKernelGGL((gemm_deep_kernel<NT_H3, EpiConvT2x2, 3>), grid, dim3(GTHREADS), 0, S(stream), x,
-                               (long long)ldx, wb, NN, amax_x, amax_w, ep, K);
+            hipLaunchKernelGGL((gemm_deep_kernel<NT_H3, DeepDenseA, EpiConvT2x2, 3>), grid, dim3(GTHREADS), 0,
+                               S(stream), DeepDenseA{x, ldx}, wb, NN, amax_x, amax_w, ep, K);
         else
-            hipLaunchKernelGGL((gemm_deep_kernel<1, EpiConvT2x2, 3>), grid, dim3(GTHREADS), 0, S(stream), x,
-                               (long long)ldx, wb, NN, amax_x, amax_w, ep, K);
+            hipLaunchKernelGGL((gemm_deep_kernel<1, DeepDenseA, EpiConvT2x2, 3>), grid, dim3(GTHREADS), 0, S(stream),
+                               DeepDenseA{x, ldx}, wb, NN, amax_x, amax_w, ep, K);
         return cdm_status();
     }
     return launch_gemm_x3<RowK<LdDenseA>::template T, StagePre, EpiConvT2x2, true>(
@@ -369,6 +369,21 @@ CDM_API int cdm_convT2x2_dgrad_x16(const float* dy, int N, int H, int W, int Cou
     if (!x16_ok(nterm) || Cin % 4 || Cout % 4 || !x16_amax_ok(nterm, amax_dy, amax_w)) return (int)hipErrorInvalidValue;
     const int M = N * H * W, K = 4 * Cout;
     EpiStore ep{dx, lddx, 0, nullptr, 1, flags, nullptr, 0, M, Cin};
+    // the two-deep prefetch form ($CDM_CONVT_DEEP=0: gemm_x3); a 16-k tile stays inside one sub-pixel (Cout % 16)
+    const char* dv = getenv("CDM_CONVT_DEEP");
+    if ((!dv || atoi(dv) != 0) && M % GBM == 0 && Cin % GBN == 0 && Cout % 16 == 0 && K % (2 * XBK) == 0 &&
+        lddy % 4 == 0 && (nterm == NT_H3 || nterm == 1)) {
+        const dim3 grid(M / GBM, Cin / GBN);
+        const __bf16* wb = reinterpret_cast<const __bf16*>(wx);
+        const DeepConvT2x2GatherA al{dy, H, W, Cout, lddy};
+        if (nterm == NT_H3)
+            hipLaunchKernelGGL((gemm_deep_kernel<NT_H3, DeepConvT2x2GatherA, EpiStore, 3>), grid, dim3(GTHREADS), 0,
+                               S(stream), al, wb, Cin, amax_dy, amax_w, ep, K);
+        else
+            hipLaunchKernelGGL((gemm_deep_kernel<1, DeepConvT2x2GatherA, EpiStore, 3>), grid, dim3(GTHREADS), 0,
+                               S(stream), al, wb, Cin, amax_dy, amax_w, ep, K);
+        return cdm_status();
+    }
     return launch_gemm_x3<RowK<LdConvT2x2GatherA>::template T, StagePre, EpiStore, true>(
         MkRowK<LdConvT2x2GatherA>{LdConvT2x2GatherA{dy, H, W, Cout, lddy, M, K}, amax_dy},
         MkPre{reinterpret_cast<const __bf16*>(wx), Cin, amax_w}, ep, M, Cin, K, 1, nterm, S(stream));

@@ -178,6 +178,23 @@ def test_convT2x2(L, N, Hin, Cin, Cout):
                             dx3.data_ptr(), Cin, Cin, 0, _s())
     torch.cuda.synchronize()
     _close(_nchw(dx3, N, Hin, Hin, Cin), xg.grad)
+    # the input gradient on the two-deep prefetch GEMM vs gemm_x3, bit for bit (plain and accumulating epilogue)
+    base = torch.randn_like(dx)
+    got = {}
+    for deep in ("1", "0"):
+        os.environ["CDM_CONVT_DEEP"] = deep
+        try:
+            for flags in (0, 2):
+                o = base.clone()
+                L.cdm_convT2x2_dgrad_h3(gyn.data_ptr(), N, Hin, Hin, Cout, Cout, wxT.data_ptr(), amg.data_ptr(),
+                                        amwT.data_ptr(), o.data_ptr(), Cin, Cin, flags, _s())
+                torch.cuda.synchronize()
+                got[deep, flags] = o
+        finally:
+            del os.environ["CDM_CONVT_DEEP"]
+    for flags in (0, 2):
+        assert torch.equal(got["1", flags], got["0", flags])
+    assert torch.equal(got["1", 0], dx3)
     if Hin % 8 == 0:
         slab.fill_(float("nan"))
         L.cdm_convT2x2_wgrad_h3(xn.data_ptr(), N, Hin, Hin, Cin, Cin, gyn.data_ptr(), Cout, Cout, amx.data_ptr(),
