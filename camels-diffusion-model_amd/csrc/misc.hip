@@ -392,7 +392,10 @@ __global__ __launch_bounds__(256) void conv_cin1_dgrad_kernel(const float* g1, i
 // FULL = false (default): 256 threads, up to HPM / 256 halo pixels per thread in the tap reduction (at 384 pixels the
 // SIMDs holding waves 0-1 do twice the FMAs of the others).  FULL ($CDM_COUT1_FULL=1): HPM threads, one halo pixel
 // each — balanced SIMDs, but same-box 182 vs 164 us per C2 step (profiles/r4_ab_cout1_threads.txt)
-template <int HPM, bool FULL = true>
+// SL: channels per LDS slab, 16 (default) or 32 ($CDM_COUT1_SLAB=32, C % 32 == 0: a pixel's slab piece is then one
+// whole 128-byte line — measured no faster, 144-149 vs 137-160 us at the bench shape, profiles/r5_cout1_probe.jsonl).
+// The tap partials st alias the slab image once the last slab is reduced (LDS 26 KiB at SL = 16).
+template <int HPM, bool FULL = true, int SL = 16>
 __global__ __launch_bounds__(FULL ? HPM : 256) void conv_cout1_fwd_band_kernel(const float* __restrict__ z, int ldz, int H, int W,
                                                                   int C, const float* __restrict__ w,
                                                                   const float* __restrict__ bias,
@@ -401,8 +404,11 @@ __global__ __launch_bounds__(FULL ? HPM : 256) void conv_cout1_fwd_band_kernel(c
                                                                   const float* __restrict__ gt) {
     constexpr int NTHR = FULL ? HPM : 256;
     constexpr int KQ = (HPM + NTHR - 1) / NTHR;       // halo pixels per thread in the tap reduction
-    __shared__ float zt[HPM * 17];                    // [halo px][16 ch + 1 pad]
-    __shared__ float st[9 * HPM];                     // [tap][halo px]
+    constexpr int PPX = SL / 4;                       // float4 pieces per halo pixel and slab
+    constexpr int ZT = HPM * (SL + 1), STN = 9 * HPM;
+    __shared__ float sm[ZT > STN ? ZT : STN];
+    float* zt = sm;                                   // [halo px][SL ch + 1 pad]
+    float* st = sm;                                   // [tap][halo px] (after the slab loop)
     const int R = 256 / W, HP = (R + 2) * W;
     // XCD-contiguous band order: the bands of an image run on one XCD, so the halo rows a band shares with its
     // neighbours come from that XCD's L2 (round-robin order fetched 1.68x the algorithmic bytes)
@@ -414,13 +420,13 @@ __global__ __launch_bounds__(FULL ? HPM : 256) void conv_cout1_fwd_band_kernel(c
     for (int k = 0; k < KQ; ++k)
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[k][t] = 0.f;
-    // staging: piece i of this thread = (halo pixel q4>>2, channels 4(q4&3)..+3) of the current 16-channel slab;
-    // the next slab's pieces are loaded into registers while this slab is reduced (one slab of latency hidden)
-    constexpr int PQ = HPM * 4 / NTHR;               // HPM * 4 pieces over the threads
+    // staging: piece i of this thread = (halo pixel q4 / PPX, channels 4 (q4 % PPX)..+3) of the current slab;
+    // the next slabs' pieces are loaded into registers while this slab is reduced
+    constexpr int PQ = HPM * PPX / NTHR;              // HPM * PPX pieces over the threads
     const float* src[PQ];
 #pragma unroll
     for (int i = 0; i < PQ; ++i) {
-        const int q4 = tid + i * NTHR, q = q4 >> 2, part = q4 & 3;
+        const int q4 = tid + i * NTHR, q = q4 / PPX, part = q4 % PPX;
         const int hh = h0 - 1 + q / W, ww = q - (q / W) * W;
         src[i] = (q < HP && (unsigned)hh < (unsigned)H) ? z + (((long long)n * H + hh) * W + ww) * ldz + part * 4
                                                         : nullptr;
@@ -434,45 +440,53 @@ __global__ __launch_bounds__(FULL ? HPM : 256) void conv_cout1_fwd_band_kernel(c
     };
     auto slab = [&](const float4 (&cur)[PQ], float4 (&nxt)[PQ], int c0) {
         float ks[4] = {1.f, 1.f, 1.f, 1.f}, kt[4] = {0.f, 0.f, 0.f, 0.f};
-        if (gs) {   // this thread's 4 channels (q4 & 3 == tid & 3 for every piece)
-            const int cb = n * C + c0 + (tid & 3) * 4;
+        if (gs) {   // this thread's 4 channels (q4 % PPX == tid % PPX for every piece)
+            const int cb = n * C + c0 + (tid % PPX) * 4;
 #pragma unroll
             for (int j = 0; j < 4; ++j) { ks[j] = gs[cb + j]; kt[j] = gt[cb + j]; }
         }
 #pragma unroll
         for (int i = 0; i < PQ; ++i) {
             const int q4 = tid + i * NTHR;
-            if ((q4 >> 2) < HP) {
+            if (q4 / PPX < HP) {
                 float v[4] = {cur[i].x, cur[i].y, cur[i].z, cur[i].w};
                 if (gs && src[i]) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) v[j] = relu_f(fmaf(v[j], ks[j], kt[j]));
                 }
-                float* d = zt + (q4 >> 2) * 17 + (q4 & 3) * 4;
+                float* d = zt + (q4 / PPX) * (SL + 1) + (q4 % PPX) * 4;
                 d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
             }
         }
         __syncthreads();
-        if (c0 + 32 < C) gload(nxt, c0 + 32);    // cur's registers are free: the slab after next
+        if (c0 + 2 * SL < C) gload(nxt, c0 + 2 * SL);    // cur's registers are free: the slab after next
 #pragma unroll
         for (int k = 0; k < KQ; ++k) {
             const int q = tid + k * NTHR;
             if (q < HP) {
 #pragma unroll
-                for (int c = 0; c < 16; ++c) {
-                    const float v = zt[q * 17 + c];
+                for (int c = 0; c < SL; ++c) {
+                    const float v = zt[q * (SL + 1) + c];
+                    // taps in pairs on the packed fp32 FMA (v_pk_fma_f32: the same fmaf per element, half the
+                    // VALU issue; the reduction is VALU-bound on the SIMDs whose waves hold two halo pixels)
+                    const float* wc = w + (c0 + c) * 9;
 #pragma unroll
-                    for (int t = 0; t < 9; ++t) acc[k][t] = fmaf(v, w[(c0 + c) * 9 + t], acc[k][t]);
+                    for (int t = 0; t < 8; t += 2) {
+                        const f32x2 r = __builtin_elementwise_fma(f32x2{v, v}, f32x2{wc[t], wc[t + 1]},
+                                                                  f32x2{acc[k][t], acc[k][t + 1]});
+                        acc[k][t] = r[0]; acc[k][t + 1] = r[1];
+                    }
+                    acc[k][8] = fmaf(v, wc[8], acc[k][8]);
                 }
             }
         }
         __syncthreads();
     };
     gload(pre[0], 0);
-    if (16 < C) gload(pre[1], 16);
-    for (int c0 = 0; c0 < C; c0 += 32) {       // C % 16 == 0 (host check)
+    if (SL < C) gload(pre[1], SL);
+    for (int c0 = 0; c0 < C; c0 += 2 * SL) {   // C % SL == 0 (host check)
         slab(pre[0], pre[0], c0);
-        if (c0 + 16 < C) slab(pre[1], pre[1], c0 + 16);
+        if (c0 + SL < C) slab(pre[1], pre[1], c0 + SL);
     }
 #pragma unroll
     for (int k = 0; k < KQ; ++k) {
@@ -1156,6 +1170,15 @@ static int launch_cout1_band(const float* z, int ldz, int N, int H, int W, int C
     const dim3 grid(N * (H / (256 / W)));
     const int hp = (256 / W + 2) * W;           // halo pixels of a band
     static const int full = [] { const char* e = getenv("CDM_COUT1_FULL"); return e ? atoi(e) : 0; }();
+    // 32-channel slabs on request ($CDM_COUT1_SLAB=32, read per call for A/B tests; not for 768-pixel bands: spills)
+    const char* sv = getenv("CDM_COUT1_SLAB");
+    if (!full && C % 32 == 0 && hp <= 512 && sv && atoi(sv) == 32) {
+        if (hp <= 384)
+            hipLaunchKernelGGL((conv_cout1_fwd_band_kernel<384, false, 32>), grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
+        else
+            hipLaunchKernelGGL((conv_cout1_fwd_band_kernel<512, false, 32>), grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);
+        return cdm_status();
+    }
     if (!full) {
         if (hp <= 384)
             hipLaunchKernelGGL((conv_cout1_fwd_band_kernel<384, false>), grid, dim3(256), 0, st, z, ldz, H, W, C, w, bias, out, gs, gt);

@@ -784,3 +784,33 @@ def test_bn_bwd_dy_pass_bit_exact(L, dt):
     torch.cuda.synchronize()
     want = ref.bfloat16() if dt & 2 else ref
     assert torch.equal(out, want)
+
+
+@pytest.mark.parametrize("N,H,C", [(2, 64, 128), (3, 32, 64), (2, 128, 32), (1, 16, 48)])
+def test_conv_cout1_band(L, N, H, C):
+    """out.3's C_out = 1 conv (the band kernel: a block stages 256 / W output rows' halo, C channels per slab through
+    LDS) vs F.conv2d in fp32, plain and with out.1's GroupNorm + ReLU applied while staging; the 32-channel slab form
+    ($CDM_COUT1_SLAB=32, C % 32 == 0) bit-identical to the default 16-channel form."""
+    torch.manual_seed(5)
+    z = torch.randn(N, C, H, H); w = torch.randn(1, C, 3, 3) * 0.1; b = torch.randn(1)
+    gs = torch.rand(N, C) + 0.5; gt = torch.randn(N, C) * 0.1
+    ref = F.conv2d(z, w, b, padding=1)
+    ref_gn = F.conv2d(torch.relu(z * gs[:, :, None, None] + gt[:, :, None, None]), w, b, padding=1)
+    zn = _nhwc(z)
+    w9 = w.reshape(C, 9).contiguous().cuda(); bc = b.cuda(); gsc = gs.contiguous().cuda(); gtc = gt.contiguous().cuda()
+    outs = {}
+    for sl in ("32", "16"):
+        os.environ["CDM_COUT1_SLAB"] = sl
+        try:
+            o = torch.empty(N, 1, H, H, device="cuda"); og = torch.empty_like(o)
+            assert L.cdm_conv3x3_cout1_fwd(zn.data_ptr(), C, N, H, H, C, w9.data_ptr(), bc.data_ptr(), o.data_ptr(),
+                                           _s()) == 0
+            assert L.cdm_conv3x3_cout1_fwd_gn(zn.data_ptr(), C, N, H, H, C, gsc.data_ptr(), gtc.data_ptr(),
+                                              w9.data_ptr(), bc.data_ptr(), og.data_ptr(), _s()) == 0
+            torch.cuda.synchronize()
+            outs[sl] = (o.cpu(), og.cpu())
+        finally:
+            del os.environ["CDM_COUT1_SLAB"]
+    _close(outs["32"][0], ref)
+    _close(outs["32"][1], ref_gn)
+    assert torch.equal(outs["32"][0], outs["16"][0]) and torch.equal(outs["32"][1], outs["16"][1])
