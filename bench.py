@@ -333,12 +333,18 @@ def train_rate(nf: int, H: int, T: int, B: int, math: str, steps: int, warmup: i
     c = torch.rand(B, NCF, device="cuda", generator=g)        # synthetic normalised parameters
     for _ in range(warmup):
         trainer.step(x0, c)
+    # one HIP event after every step on the launch stream (recording one does not synchronise): the per-step GPU times
+    # whose median BASELINE.md §3 names; the contract's value stays the barrier-bracketed K-step span
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     barrier()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    evs[0].record()
+    for k in range(steps):
         trainer.step(x0, c)
+        evs[k + 1].record()
     barrier()
     dt = time.perf_counter() - t0
+    step_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(steps)]
     loss = float(trainer.loss.item())
     if dist is not None:
         tt = torch.tensor([dt], device="cuda")
@@ -347,9 +353,39 @@ def train_rate(nf: int, H: int, T: int, B: int, math: str, steps: int, warmup: i
     conv = time_dominant_conv_in_step(trainer, x0, c) if conv_probe else None
     del trainer
     model.eval()
+    train_rate.last_step_ms = step_ms
     if conv_probe:
         return model, dt / steps * 1e3, loss, conv
     return model, dt / steps * 1e3, loss
+
+
+def step_stats(step_ms):
+    """Median / min / max of the per-step GPU times (HIP events), ms."""
+    if not step_ms:
+        return None
+    v = sorted(step_ms)
+    n = len(v)
+    med = v[n // 2] if n % 2 else 0.5 * (v[n // 2 - 1] + v[n // 2])
+    return {"median_ms": round(med, 3), "min_ms": round(v[0], 3), "max_ms": round(v[-1], 3), "steps": n,
+            "measured": "HIP events recorded after every timed step on the launch stream"}
+
+
+def whole_path_rooflines(math: str, B: int, ms_step: float, n: int, sample_ms: dict):
+    """Whole-path fractions of the conv arithmetic's ceiling (north_star: training-step and T=1500 sampling throughput
+    as achieved roofline fractions): the algorithmic fp32-equivalent FLOPs (forward 19.178788 GFLOP/img,
+    train step 3x) over the measured time, against the ceiling of the arithmetic the 3x3 convs run in (h3: 2.5 PF/s / 3
+    products; bf16: 2.5 PF/s; fp32: the fp32 MFMA peak).  sample_ms: {"w=0": ms per denoise step, "w=1": ..., ...}; a
+    CFG step runs the 2n-image forward.  The non-conv FLOPs (~1 %) count as if they ran at that ceiling too."""
+    peak = PEAK_BF16_TFLOPS if math == "bf16" else conv_peak(math)
+    tr = 3 * FWD_GFLOP_PER_IMG * B / (ms_step * 1e-3) / 1e3
+    out = {"train_step": {"achieved": round(tr, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
+                          "frac": round(tr / peak, 4), "gflop_per_img": round(3 * FWD_GFLOP_PER_IMG, 4)}}
+    for k, ms in sample_ms.items():
+        imgs = n if k == "w=0" else 2 * n
+        a = FWD_GFLOP_PER_IMG * imgs / (ms * 1e-3) / 1e3
+        out[f"sample_{k}"] = {"achieved": round(a, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
+                              "frac": round(a / peak, 4), "forward_images_per_step": imgs}
+    return out
 
 
 def extra_configs(args, barrier):
@@ -358,6 +394,7 @@ def extra_configs(args, barrier):
     out = {}
     # C4: bf16 MFMA operands, fp32 accumulate / master weights / activations; CFG w in {0,1,3}
     model, ms, loss, (cms4, cn4) = train_rate(NF, H, T, args.batch, "bf16", 10, 3, 0, barrier, conv_probe=True)
+    c4_steps = step_stats(getattr(train_rate, "last_step_ms", None))
     _progress(f"C4 train {ms:.3f} ms/step")
     c4_tf = CONV_GFLOP_PER_IMG * args.batch / (cms4 * 1e-3) / 1e3
     c4 = {"workload": "C4: ContextUnet n_feat=128 64x64, bf16 mixed-precision convs (bf16 operands, fp32 "
@@ -376,6 +413,9 @@ def extra_configs(args, barrier):
         c4["sample"][f"w={w:g}"] = {"ms_per_denoise_step": round(sms, 3), "steps_run": S,
                                    "img_per_s": round(args.sample_batch / (sms * 1e-3 * T), 4),
                                    "extrapolated_to_T": S < T}
+    c4["train_step_stats"] = c4_steps
+    c4["whole_path_roofline"] = whole_path_rooflines(
+        "bf16", args.batch, ms, args.sample_batch, {k: v["ms_per_denoise_step"] for k, v in c4["sample"].items()})
     out["c4_bf16_cfg"] = c4
     del model
     torch.cuda.empty_cache()
@@ -589,6 +629,7 @@ def main():
                                                          barrier, use_graph=not args.no_graph, dist=dist,
                                                          conv_probe=True)
     train_ips = world * B / (ms_step * 1e-3)
+    c2_steps = step_stats(getattr(train_rate, "last_step_ms", None))
     _progress(f"C2 train {ms_step:.3f} ms/step")
 
     # ---------------- sampling (replicas) ----------------
@@ -614,6 +655,8 @@ def main():
 
     extra = extra_configs(args, barrier) if (world == 1 and not args.no_extra) else None
 
+    wp = whole_path_rooflines(args.conv_math, B, ms_step, n,
+                              {"w=0": sms, **{k: v["ms_per_denoise_step"] for k, v in cfg.items()}})
     out = None
     if rank == 0:
         out = {
@@ -655,8 +698,11 @@ def main():
                                            f"{CONV_MATH_INFO[args.conv_math][0]} products per fp32 MAC"),
                          "vs_fp32_mfma_peak": round(conv_tflops / PEAK_FP32_TFLOPS, 4)},
             "train_tflops_per_gpu": round(3 * FWD_GFLOP_PER_IMG * B / (ms_step * 1e-3) / 1e3, 2),
+            "train_step_stats": c2_steps,
+            "whole_path_roofline": wp,
             "final_loss": loss,
         }
+        out["sample"]["roofline"] = {k[len("sample_"):]: v for k, v in wp.items() if k.startswith("sample_")}
         if extra:
             out["configs"] = extra
         if logged:

@@ -901,7 +901,7 @@ CDM_API int cdm_bn_bwd_dy(const void* g, int ldg, const void* y, int ldy, long l
                           const float* t, const float* mean, const float* invstd, const float* A, const float* B,
                           const float* Cc, void* dy, int lddy, int dt, void* stream) {
     // dt bit 0: g and y are bf16, bit 1: dy is stored as bf16
-    if (C % 8 || 256 % (C / 8) || ldg % 8 || ldy % 8 || lddy % 8 || P < 0) return (int)hipErrorInvalidValue;
+    if (C <= 0 || C % 8 || 256 % (C / 8) || ldg % 8 || ldy % 8 || lddy % 8 || P < 0) return (int)hipErrorInvalidValue;
     if (P == 0) return 0;
     const int nb = ew_blocks(P * (C / 8));
     auto run = [&](auto gtag, auto otag) {

@@ -10,13 +10,14 @@ whole by :class:`cdm_amd.engine.UNetEngine`, and a block called on its own runs 
 The reference draws a *fresh* random 1x1 shortcut convolution on every forward call
 (diffusion_utilities.py:54).  ``shortcut_source`` selects where that draw comes from:
 ``"cpu"`` (default) consumes the CPU torch RNG exactly as the reference does (bit-compatible
-seeding), ``"device"`` draws the same U(-1, 1) distribution from on-device Philox (no host work;
+seeding), ``"device"`` draws the same U(-1/sqrt(C), 1/sqrt(C)) distribution (C = in_channels) from on-device
+Philox (no host work;
 used by the captured train/sample loops).
 """
 from __future__ import annotations
 
 import itertools
-
+import math
 import os
 from typing import Dict, List, Optional
 
@@ -274,7 +275,10 @@ class ContextUnet(nn.Module):
         nw = n_sets * nf * self.in_channels
         w = torch.empty(nw + n_sets * nf, device=device)
         self._sc_counter += 1
-        lib().cdm_philox_uniform(w.data_ptr(), w.numel(), -1.0, 1.0, 0x5C0FFEE + id(self) % 65536,
+        # the reference's fresh nn.Conv2d(C, n_feat, 1) draws weight (kaiming_uniform_, a = sqrt(5)) and bias both from
+        # U(-1/sqrt(fan_in), 1/sqrt(fan_in)), fan_in = C: U(-1, 1) for the single-channel maps
+        bound = 1.0 / math.sqrt(self.in_channels)
+        lib().cdm_philox_uniform(w.data_ptr(), w.numel(), -bound, bound, 0x5C0FFEE + id(self) % 65536,
                                  self._sc_counter, None, _stream())
         return w[:nw], w[nw:]
 

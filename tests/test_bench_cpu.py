@@ -35,6 +35,25 @@ def test_pmc_traffic_missing_keys(tmp_path, monkeypatch):
     assert b.pmc_traffic("h3") == int((10 / b.HALO_FETCH_PER_BYTE + 2) * 1024)
 
 
+def test_whole_path_rooflines_and_step_stats():
+    """The bench line's whole-path fractions (north_star: train-step and T=1500 sampling throughput as roofline
+    fractions) and the median step, on round 5's driver numbers: C2 47.988 ms per 256-image step ->
+    0.368 of the h3 ceiling; sampling 12.961 ms per denoise step at n = 256 -> 0.455; a CFG step runs 2n images."""
+    b = _bench()
+    wp = b.whole_path_rooflines("h3", 256, 47.988, 256, {"w=0": 12.961, "w=3": 25.0})
+    assert abs(wp["train_step"]["frac"] - 0.3682) < 2e-3
+    assert abs(wp["sample_w=0"]["frac"] - 0.4546) < 2e-3
+    assert wp["sample_w=3"]["forward_images_per_step"] == 512
+    assert abs(wp["sample_w=3"]["achieved"] - 2 * wp["sample_w=0"]["achieved"] * 12.961 / 25.0) < 0.05
+    assert wp["train_step"]["peak"] == round(2500.0 / 3, 2)
+    c4 = b.whole_path_rooflines("bf16", 256, 26.408, 256, {"w=0": 7.0})
+    assert c4["train_step"]["peak"] == 2500.0 and abs(c4["train_step"]["frac"] - 0.2231) < 2e-3
+    st = b.step_stats([3.0, 1.0, 2.0, 10.0])
+    assert st["median_ms"] == 2.5 and st["min_ms"] == 1.0 and st["max_ms"] == 10.0 and st["steps"] == 4
+    assert b.step_stats([4.0, 1.0, 2.0])["median_ms"] == 2.0
+    assert b.step_stats([]) is None
+
+
 def _run_bench(*args, env_extra=None, timeout=240):
     import json
     import subprocess

@@ -134,6 +134,94 @@ def test_in_channels_eval_forward(C, math):
     assert _rel(eps, ref) < 2e-4
 
 
+@pytest.mark.parametrize("C", [1, 3])
+def test_device_shortcut_draw_range(C):
+    """shortcut_source="device": the fresh 1x1 shortcut's weight and bias come from U(-1/sqrt(C), 1/sqrt(C)), the
+    distribution of the reference's nn.Conv2d(C, n_feat, 1) init (kaiming_uniform_(a = sqrt(5)) and its bias bound,
+    fan_in = C; diffusion_utilities.py:54).  ADVICE r5: the device draw was U(-1, 1) for every C."""
+    import cdm_amd
+    m = cdm_amd.ContextUnet(C, 128, NCF, H, shortcut_source="device").cuda()
+    bound = 1.0 / C ** 0.5
+    ws, bs = [], []
+    for _ in range(8):
+        w, b = m.draw_shortcut(torch.device("cuda"))
+        assert w.numel() == 128 * C and b.numel() == 128
+        ws.append(w.cpu()); bs.append(b.cpu())
+    w, b = torch.cat(ws), torch.cat(bs)
+    for v in (w, b):
+        assert v.abs().max().item() <= bound
+        assert v.abs().max().item() >= 0.95 * bound          # 1024+ draws reach the edge of the interval
+        assert abs(v.mean().item()) <= 0.1 * bound and abs(v.std().item() - bound / 3 ** 0.5) <= 0.1 * bound
+
+
+def test_in_channels_bf16_c4_arithmetic():
+    """C4's bf16 arithmetic with in_channels = 3 at n_feat = 128 (the cp > 1 image through the bf16 matrix
+    cores — the batched bf16 repack of the init conv, the fused BN / fused eval-epilogue paths, which need C_out % 128 ==
+    0): eval and train forward, and every gradient (parameters, x, t, c) of a train-mode call, vs fp64, within 1.5x the
+    error of the reference under C4's bf16 operand rounding (tests/_bf16emu.py; train: conv outputs / gradients stored
+    in bf16 as autocast does), the bar of tests/test_gpu_configs.py's C4 tests (max and median over tensors)."""
+    import numpy as np
+    import cdm_amd
+    from _bf16emu import _bf16_operands
+    C, nf, Hh, Bb = 3, 128, 32, 2
+    torch.manual_seed(17)
+    m = cdm_amd.ContextUnet(C, nf, NCF, Hh, conv_math="bf16").cuda()
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(71)
+    x = torch.randn(Bb, C, Hh, Hh, generator=g); t = torch.rand(Bb, generator=g); c = torch.rand(Bb, NCF, generator=g)
+    weight = torch.randn(Bb, C, Hh, Hh, generator=g)
+    sc = None
+
+    def oracle(dtype, emulate, train):
+        s = {k: (v.to(dtype) if v.is_floating_point() else v.clone()).clone() for k, v in sd.items()}
+        keys = [k for k, _, kind in R.state_dict_layout(C, nf, NCF, Hh) if kind == "param"]
+        for k in keys:
+            s[k].requires_grad_(True)
+        xx, tt, cc = (v.to(dtype).clone().requires_grad_(True) for v in (x, t, c))
+        args = dict(n_feat=nf, n_cfeat=NCF, height=Hh, train=train, shortcut=(sc[0].to(dtype), sc[1].to(dtype)))
+        if emulate:
+            with _bf16_operands(outputs=train):
+                eps = R.unet_forward(s, xx, tt, cc, **args)
+                (eps * weight.to(dtype)).sum().backward()
+        else:
+            eps = R.unet_forward(s, xx, tt, cc, **args)
+            (eps * weight.to(dtype)).sum().backward()
+        return eps.detach(), {"x": xx.grad, "t": tt.grad, "c": cc.grad, **{k: s[k].grad for k in keys}}
+
+    res = {}
+    for train in (False, True):
+        m.load_state_dict(sd)
+        m.train(train)
+        # the module draws its shortcut from the CPU RNG (shortcut_source="cpu"): the oracle replays that draw
+        torch.manual_seed(99)
+        sc = R.draw_shortcut(C, nf)
+        torch.manual_seed(99)
+        if train:
+            xg, tg, cg = (v.cuda().requires_grad_(True) for v in (x, t, c))
+            eps = m(xg, tg, cg)
+            (eps * weight.cuda()).sum().backward()
+            hip = {"x": xg.grad, "t": tg.grad, "c": cg.grad, **{k: p.grad for k, p in m.named_parameters()}}
+        else:
+            with torch.no_grad():
+                eps = m(x.cuda(), t.cuda(), c.cuda())
+        e64, g64 = oracle(torch.float64, False, train)
+        ee, ge = oracle(torch.float32, True, train)
+        res[f"eps_{'train' if train else 'eval'}"] = (_rel(eps.detach(), e64), _rel(ee, e64))
+        if train:
+            per = {}
+            for k, ref in g64.items():
+                if ".conv1.0.bias" in k or ".conv2.0.bias" in k:
+                    continue
+                per[k] = (_rel(hip[k], ref), _rel(ge[k], ref))
+            gh, gm = [v[0] for v in per.values()], [v[1] for v in per.values()]
+            res["grad_max"] = (max(gh), max(gm))
+            res["grad_median"] = (float(np.median(gh)), float(np.median(gm)))
+            print("worst tensors (HIP, emulated):", sorted(per.items(), key=lambda kv: -kv[1][0])[:6])
+    print("in_channels=3 bf16 (HIP, bf16-emulated reference):", res)
+    for k, (h, e) in res.items():
+        assert h <= 1.5 * e, (k, h, e)
+
+
 def test_in_channels_single_channel_loops_raise():
     """the training loop and samplers (reference: in_channels = 1, [n, 1, H, W] draws) refuse other channel counts"""
     import cdm_amd

@@ -197,23 +197,40 @@ def _golden_ddpm(m, T):
 
 
 def _trajectory_check(name, sfx, x, inter, w, **rec):
-    """final / per-snapshot deviations from fp64 of HIP and of the golden's fp32 reference; 1.5x bar"""
+    """final / per-snapshot deviations from fp64 of HIP and of the golden's fp32 reference; 1.5x bar.
+
+    Second bar: the direct distance max|x_HIP - x_golden32| / max|x_fp64| at every point.  HIP replays the
+    golden's draws, schedule and coefficient tables, and its denoise update is bit-identical to the reference's fp32
+    ops, so both runs share the update's rounding at |x| ~ 1e4 — which can dominate both deviations from fp64 (w = 0:
+    HIP's equals the golden's to all digits at most snapshots) and hide the network's own error under it.  The direct
+    distance cancels that shared term and is the network's error (HIP's vs the reference's fp32 summation order): it
+    must stay within the golden's own deviation from fp64 at that point.  Except at the first snapshot (slot 0, the x
+    after step i = T): both runs start from the same x_T, there is no shared update rounding yet, the deviation from
+    fp64 IS the network's error and the 1.5x bar holds it directly, while the direct distance between two independent
+    network errors of that size reaches up to ~1.4x either (measured 1.21-1.24e-7 vs the golden's 0.90-0.96e-7 at
+    w = 3, round 6)."""
     ref64 = sfx[f"w{w:g}_x_fp64"]
     mx = np.abs(ref64).max()
 
     def dev(a, r):
-        return float(np.abs(np.asarray(a, np.float64) - r).max() / np.abs(r).max())
-    rows = [("final", dev(x, ref64), dev(sfx[f"w{w:g}_x"], ref64))]
+        return float(np.abs(np.asarray(a, np.float64) - np.asarray(r, np.float64)).max() / np.abs(r).max())
+    rows = [("final", dev(x, ref64), dev(sfx[f"w{w:g}_x"], ref64),
+             dev(x, sfx[f"w{w:g}_x"]) * np.abs(sfx[f"w{w:g}_x"]).max() / mx)]
     for j, sl in enumerate(sfx["snap_keep"]):
         r = sfx[f"w{w:g}_inter_fp64"][j]
-        rows.append((int(sl), dev(inter[sl], r), dev(sfx[f"w{w:g}_inter"][j], r)))
-    print(f"{name} w={w:g} {rec}: max|x| {mx:.3g}; deviation from fp64 HIP / golden reference fp32: "
-          + " ".join(f"{a}:{b:.2e}/{c:.2e}" for a, b, c in rows))
+        g32 = sfx[f"w{w:g}_inter"][j]
+        rows.append((int(sl), dev(inter[sl], r), dev(g32, r),
+                     float(np.abs(np.asarray(inter[sl], np.float64) - g32).max() / np.abs(r).max())))
+    print(f"{name} w={w:g} {rec}: max|x| {mx:.3g}; deviation from fp64 HIP / golden reference fp32 / direct HIP-golden: "
+          + " ".join(f"{a}:{b:.2e}/{c:.2e}/{d:.2e}" for a, b, c, d in rows))
     _parity.record(name, w=w, max_abs_x=float(mx), final_err=rows[0][1], final_err_ref32=rows[0][2],
-                   worst_ratio=max(b / c for _, b, c in rows),
-                   snapshots=[{"slot": a, "err": b, "err_ref32": c} for a, b, c in rows[1:]], **rec)
-    for a, b, c in rows:
+                   final_direct=rows[0][3], worst_ratio=max(b / c for _, b, c, _ in rows),
+                   worst_direct_ratio=max(d / c for _, _, c, d in rows),
+                   snapshots=[{"slot": a, "err": b, "err_ref32": c, "direct": d} for a, b, c, d in rows[1:]], **rec)
+    for a, b, c, d in rows:
         assert b <= 1.5 * c, f"{name} w={w:g} at {a}: HIP {b:.3e} vs reference {c:.3e}"
+        if a != 0:
+            assert d <= c, f"{name} w={w:g} at {a}: direct distance HIP - golden {d:.3e} > golden's deviation {c:.3e}"
 
 
 @pytest.mark.parametrize("w,math", [(0.0, "h3"), (0.0, "fp32"), (3.0, "h3")])
