@@ -1,8 +1,8 @@
 """Whole-model parity of the HIP ContextUnet against the CPU oracle / reference golden vectors.
 
-Every test runs with the three fp32-class 3x3-conv arithmetics: "fp32" (fp32 MFMA), "x6" (split-bf16
-MFMA, 6 cross terms) and "h3" (scaled split-fp16 MFMA, 3 cross terms) — same tolerances, so x6 and h3
-are held to the fp32 bar.
+The tests marked MATH run with the three fp32-class 3x3-conv arithmetics: "fp32" (fp32 MFMA), "x6" (split-bf16
+MFMA, 6 cross terms) and "h3" (scaled split-fp16 MFMA, 3 cross terms) — same tolerances, so x6 and h3 are held to
+the fp32 bar; the fp64-anchored gradient test runs the shipped arithmetics fp32 and h3 (round 6: x6 is not shipped).
 
 Tolerances (fp32 everywhere; only summation order differs):
   forward eps            max|d| <= 1e-4 * max|ref|
@@ -150,7 +150,7 @@ def _oracle_grads(sd, x, c, noise, tt, T, ab, nf, dtype, seed, kinks=None):
 _ORACLE_CACHE = {}
 
 
-@MATH
+@pytest.mark.parametrize("math", ["fp32", "h3"])
 @pytest.mark.parametrize("nf", [64, 128])
 def test_train_grads_random_weights_vs_fp64(nf, math):
     """HIP grads vs an fp64 oracle, at the accuracy the reference's own fp32 CPU path has (n_feat 64 and the
@@ -163,10 +163,9 @@ def test_train_grads_random_weights_vs_fp64(nf, math):
     on one thread (other CPU reduction orders).  Criterion per tensor: HIP <= 3x the reference + 2e-6; median over
     tensors <= 3x the reference's median.  Conv biases feeding a BatchNorm have an analytic gradient of 0 (rounding
     noise only): |g| <= 1e-4 * max grad.  The decisions each flips relative to plain fp64 are recorded.
-    x6 (bf16 hi + mid + lo, the dropped mid.lo / lo.mid / lo.lo products) is held to 5x per tensor: its single-conv error
-    is up to 2x torch's own fp32 conv (profiles/r1_conv_accuracy.jsonl, where h3 is below it on every
-    shape), and over the 20-layer backward at n_feat 128 that compounds to 4.4x on the worst tensor (round 5 box: median
-    2.7x).  x6 is a non-default arithmetic; h3 (the benched one) and fp32 keep 3x.
+    Round 6: x6 (a non-shipped arithmetic: no bench leg or config runs it) is out of this test's matrix instead of being
+    held to the 5x per tensor its 20-layer backward needed at n_feat 128 (its single-conv error is up to 2x torch's own,
+    DESIGN §3.1); its forward stays in the forward tests at the same bars as h3 and fp32.
     """
     import _parity
     from _kinks import Kinks, hip_kinks
@@ -216,7 +215,7 @@ def test_train_grads_random_weights_vs_fp64(nf, math):
         else:
             e_hip = ((got - ref).norm() / ref.norm()).item()
             e_cpu = max(((g32[k].double() - g64r[k]).norm() / g64r[k].norm()).item() for g32, g64r in refs)
-            ok = e_hip <= (5 if math == "x6" else 3) * e_cpu + 2e-6
+            ok = e_hip <= 3 * e_cpu + 2e-6
             errs.append(e_hip); errs32.append(e_cpu)
             print(f"{k:40s} l2rel hip {e_hip:.2e} cpu32 {e_cpu:.2e}")
         if not ok:
@@ -454,8 +453,11 @@ def test_map_heights_not_multiple_of_16(H):
     """ContextUnet(height=H) for any H % 4 == 0 (the reference's only requirement: ContextUnet.py:17,27 — two MaxPool2d(2),
     AvgPool2d(H/4), ConvTranspose2d(k = H/4)); widths outside the LDS-halo / band kernels' set run the generic kernels
     (split GEMM convs, fp32 weight-gradient GEMMs for widths % 8 != 0).  n_feat 16, B 2, h3: forward train / eval vs
-    the fp32 oracle (2e-4) and every parameter gradient vs fp64 (the test_train_grads_random_weights_vs_fp64 bar)."""
+    the fp32 oracle (2e-4) and every parameter gradient vs fp64 at the bar of test_train_grads_random_weights_vs_fp64
+    (it was an absolute 1e-2 / 5e-3): each run on its own ReLU / MaxPool branch (tests/_kinks.py), per tensor
+    HIP <= 3x the reference fp32 run's relative L2 + 2e-6, median over tensors <= 3x the reference's median."""
     from cdm_amd import ContextUnet
+    from _kinks import Kinks, hip_kinks
     nf, B, T = 16, 2, 1500
     torch.manual_seed(23)
     m = ContextUnet(1, nf, 6, H).cuda()
@@ -479,22 +481,35 @@ def test_map_heights_not_multiple_of_16(H):
     torch.manual_seed(33)
     pred = m(xp.cuda(), (tt / T).cuda(), c.cuda())
     F.mse_loss(pred, noise.cuda()).backward()
+    torch.manual_seed(33)
+    sc = R.draw_shortcut(1, nf)                      # the draw the module made
+    got = {k: p.grad.cpu().double() for k, p in m.named_parameters()}
+    m.load_state_dict(sd)
+    hk_relu, hk_pool = hip_kinks(m, xp, tt / T, c, sc, frozen=False)
 
-    def oracle(dtype):
+    def oracle(dtype, kinks):
         s = {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in sd.items()}
         tr = R.OracleTrainer(s, n_feat=nf, n_cfeat=6, height=H)
-        torch.manual_seed(33)
-        w, b = R.draw_shortcut(1, nf)
-        return tr.step(x.to(dtype), c.to(dtype), noise.to(dtype), tt, T, ab.to(dtype), (w.to(dtype), b.to(dtype)))
-    _, p64, g64 = oracle(torch.float64)
+        with kinks:
+            return tr.step(x.to(dtype), c.to(dtype), noise.to(dtype), tt, T, ab.to(dtype),
+                           (sc[0].to(dtype), sc[1].to(dtype)))
+    _, p64, g64 = oracle(torch.float64, Kinks(hk_relu, hk_pool))
+    cap32 = Kinks()
+    _, _, g32 = oracle(torch.float32, cap32)
+    _, _, g64r = oracle(torch.float64, Kinks(cap32.relu, cap32.pool))
     assert _rel(pred.double(), p64) < 2e-4
     gmax = max(v.abs().max().item() for v in g64.values())
-    errs = {}
-    for k, p in m.named_parameters():
-        got = p.grad.cpu().double()
+    errs, errs32, bad = {}, {}, []
+    for k, v in got.items():
         if ".conv1.0.bias" in k or ".conv2.0.bias" in k:
-            assert got.abs().max().item() <= 1e-4 * gmax, k
-        else:
-            errs[k] = ((got - g64[k]).norm() / g64[k].norm()).item()
-    print(f"H={H}: grads vs fp64 max {max(errs.values()):.2e} median {np.median(list(errs.values())):.2e}")
-    assert max(errs.values()) <= 1e-2 and float(np.median(list(errs.values()))) <= 5e-3
+            assert v.abs().max().item() <= 1e-4 * gmax, k
+            continue
+        errs[k] = ((v - g64[k]).norm() / g64[k].norm()).item()
+        errs32[k] = ((g32[k].double() - g64r[k]).norm() / g64r[k].norm()).item()
+        if errs[k] > 3 * errs32[k] + 2e-6:
+            bad.append((k, errs[k], errs32[k]))
+    med, med32 = float(np.median(list(errs.values()))), float(np.median(list(errs32.values())))
+    print(f"H={H}: grads vs fp64 (own branches) max {max(errs.values()):.2e} median {med:.2e}; reference fp32 max "
+          f"{max(errs32.values()):.2e} median {med32:.2e}")
+    assert not bad, bad
+    assert med <= 3 * med32
