@@ -63,6 +63,15 @@ CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int C
         case 16: CDM_ABL(16); break;
         case 32: CDM_ABL(32); break;
         case 17: CDM_ABL(17); break;
+        case 3: CDM_ABL(3); break;
+        case 5: CDM_ABL(5); break;
+        case 9: CDM_ABL(9); break;
+        case 13: CDM_ABL(13); break;
+        case 21: CDM_ABL(21); break;
+        case 25: CDM_ABL(25); break;
+        case 29: CDM_ABL(29); break;
+        case 33: CDM_ABL(33); break;
+        case 45: CDM_ABL(45); break;
         case 60: CDM_ABL(60); break;
         case 61: CDM_ABL(61); break;
         case 62: CDM_ABL(62); break;

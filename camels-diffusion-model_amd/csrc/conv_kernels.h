@@ -829,6 +829,42 @@ static __device__ __forceinline__ void split_terms(const float (&x)[E], float sc
     }
 }
 
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+// h3 split of the pair (a, b), packed as the LDS images hold it (low half = a): hi = f16(sc x), lo = f16(sc x - hi),
+// each by one v_fma_mix{lo,hi}_f16 that forms the scaled product inside the instruction and writes its packed half
+// directly: 4 VALU per pair.  The compiler's own code for split_terms<NT_H3> + packing rounded hi twice (a mix for the
+// residual, a v_cvt_pk_f16_f32 of two separately multiplied products for the store: 7 VALU per pair; round 6).  The
+// same roundings (sc x is exact: sc is a power of two; each term is one RNE fp16 rounding of an exact fma), so the
+// terms are bit-identical to split_terms<NT_H3> except hi(-0) = +0 (value-equal).
+static __device__ __forceinline__ void h3_pair(float a, float b, float sc, unsigned& hp, unsigned& lp) {
+    asm("v_fma_mixlo_f16 %0, %2, %3, 0\n\t"
+        "v_fma_mixhi_f16 %0, %2, %4, 0\n\t"
+        "v_fma_mixlo_f16 %1, %2, %3, -%0 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %1, %2, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(hp), "=&v"(lp)
+        : "v"(sc), "v"(a), "v"(b));
+}
+
+// x[0..3] (4 consecutive k of one row) -> its NS term images, 2 elements per dword: t[term] = {k0 | k1, k2 | k3}
+template <int NT>
+static __device__ __forceinline__ void split_pk4(const float (&x)[4], float sc, u32x2 (&t)[3]) {
+    if constexpr (NT == NT_H3) {
+        unsigned h0, h1, l0, l1;
+        h3_pair(x[0], x[1], sc, h0, l0);
+        h3_pair(x[2], x[3], sc, h1, l1);
+        t[0] = u32x2{h0, h1};
+        t[1] = u32x2{l0, l1};
+    } else {
+        constexpr int NS = XTerms<NT>::NS;
+        __bf16 h[4], m[4], l[4];
+        split_terms<NT>(x, sc, h, m, l);
+        t[0] = __builtin_bit_cast(u32x2, bf16x4{h[0], h[1], h[2], h[3]});
+        if constexpr (NS > 1) t[1] = __builtin_bit_cast(u32x2, bf16x4{m[0], m[1], m[2], m[3]});
+        if constexpr (NS > 2) t[2] = __builtin_bit_cast(u32x2, bf16x4{l[0], l[1], l[2], l[3]});
+    }
+}
+
 template <class LD, int NT>
 struct StageRowK {
     static constexpr int NS = XTerms<NT>::NS;
@@ -856,12 +892,11 @@ struct StageRowK {
 #pragma unroll
         for (int i = 0; i < LDN; ++i) {
             const float x[4] = {r[i].x, r[i].y, r[i].z, r[i].w};
-            __bf16 h[4], m[4], l[4];
-            split_terms<NT>(x, sc, h, m, l);
+            u32x2 tm[3];
+            split_pk4<NT>(x, sc, tm);
             __bf16* d = base + xoff(tid / 4 + i * (GTHREADS / 4), (tid % 4) * 4);
-            *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
-            if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + XPLANE) = bf16x4{m[0], m[1], m[2], m[3]};
-            if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + 2 * XPLANE) = bf16x4{l[0], l[1], l[2], l[3]};
+#pragma unroll
+            for (int k = 0; k < NS; ++k) *reinterpret_cast<u32x2*>(d + k * XPLANE) = tm[k];
         }
     }
 };
@@ -1479,21 +1514,16 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
                 }
 #pragma unroll
                 for (int e = 0; e < 4; ++e) xv[e] = inb(j) ? xv[e] : 0.f;   // zero padding (transform not applied)
-                __bf16 h[4], m[4], l[4];
+                u32x2 tm[3];
                 if constexpr (ABL & 8) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        h[e] = __builtin_bit_cast(__bf16, (unsigned short)__float_as_uint(xv[e]));
-                        m[e] = __builtin_bit_cast(__bf16, (unsigned short)(__float_as_uint(xv[e]) >> 16));
-                        l[e] = h[e];
-                    }
+                    const u32x2 raw{__float_as_uint(xv[0]), __float_as_uint(xv[1])};
+                    tm[0] = raw; tm[1] = u32x2{__float_as_uint(xv[2]), __float_as_uint(xv[3])}; tm[2] = raw;
                 } else {
-                    split_terms<NT>(xv, sx, h, m, l);
+                    split_pk4<NT>(xv, sx, tm);
                 }
                 __bf16* d = base + hdst[j];
-                *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
-                if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + HPLANE) = bf16x4{m[0], m[1], m[2], m[3]};
-                if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + 2 * HPLANE) = bf16x4{l[0], l[1], l[2], l[3]};
+#pragma unroll
+                for (int k = 0; k < NS; ++k) *reinterpret_cast<u32x2*>(d + k * HPLANE) = tm[k];
             }
         }
     };
@@ -1910,13 +1940,12 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
                 __bf16* base = base0 + ks * STEP;
                 const float4 v = op ? rb[ks][i] : ra[ks][i];
                 const float xv[4] = {v.x, v.y, v.z, v.w};
-                __bf16 h[4], m[4], l[4];
-                split_terms<NT>(xv, op ? sx_ : sdy_, h, m, l);
+                u32x2 tm[3];
+                split_pk4<NT>(xv, op ? sx_ : sdy_, tm);
                 const int kk = kq + 8 * i;
                 char* d = reinterpret_cast<char*>(base + op * NS * IMG) + trswz(kk, c4 >> 3) + (c4 & 7) * 2;
-                *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
-                if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + IMG * 2) = bf16x4{m[0], m[1], m[2], m[3]};
-                if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + IMG * 4) = bf16x4{l[0], l[1], l[2], l[3]};
+#pragma unroll
+                for (int k = 0; k < NS; ++k) *reinterpret_cast<u32x2*>(d + k * IMG * 2) = tm[k];
             }
     };
     // transposed-read addresses: lane 4q+p of 16-lane group g supplies row kb+q, columns c0+4p..+3
@@ -2125,12 +2154,11 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
     };
     auto put = [&](char* img, int row, const float4& v, float sc, int ielems) {
         const float xv[4] = {v.x, v.y, v.z, v.w};
-        __bf16 h[4], m[4], l[4];
-        split_terms<NT>(xv, sc, h, m, l);
+        u32x2 tm[3];
+        split_pk4<NT>(xv, sc, tm);
         char* d = img + trswz(row, c4 >> 3) + (c4 & 7) * 2;
-        *reinterpret_cast<bf16x4*>(d) = bf16x4{h[0], h[1], h[2], h[3]};
-        if constexpr (NS > 1) *reinterpret_cast<bf16x4*>(d + ielems * 2) = bf16x4{m[0], m[1], m[2], m[3]};
-        if constexpr (NS > 2) *reinterpret_cast<bf16x4*>(d + ielems * 4) = bf16x4{l[0], l[1], l[2], l[3]};
+#pragma unroll
+        for (int k = 0; k < NS; ++k) *reinterpret_cast<u32x2*>(d + k * ielems * 2) = tm[k];
     };
     // one-term bf16 operands without a staging transform are copied as they arrive (no convert round trip)
     constexpr bool RAWG = NT == 1 && !PRE::on && std::is_same<GT, __bf16>::value;
