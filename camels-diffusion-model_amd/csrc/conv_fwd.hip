@@ -72,6 +72,8 @@ CDM_API int cdm_conv3x3_halo_ablate(int abl, const float* x, int N, int H, int C
         case 29: CDM_ABL(29); break;
         case 33: CDM_ABL(33); break;
         case 45: CDM_ABL(45); break;
+        case 16385: CDM_ABL(16385); break;
+        case 16445: CDM_ABL(16445); break;
         case 60: CDM_ABL(60); break;
         case 61: CDM_ABL(61); break;
         case 62: CDM_ABL(62); break;

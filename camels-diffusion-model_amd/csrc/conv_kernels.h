@@ -1334,7 +1334,9 @@ constexpr int HTHREADS = 512;
 // 32 halo loaded for the first chunk only, 64 / 128 prefetch schedules: 2 reads per MFMA gap / all reads after the
 // tap's first MFMA, 256 staggered halo split (waves 0-3 split + store the next chunk's halo after their last kernel
 // row's MFMAs, waves 4-7 before them, so each SIMD pairs one wave's VALU with its partner's MFMAs), 512 static
-// priority 1 for waves 4-7
+// priority 1 for waves 4-7, 16384 epilogue skipped (behind a never-taken branch: the MFMAs stay live; round 6: 0.753 ->
+// 0.672 ms at 16 tiles per block — the epilogue's 537 MB of y, stored by every block at the same time, drains at ~6.6
+// TB/s with no MFMA running; issuing the next chunk's loads ahead of those stores measured slower, 0.822 -> 0.833 ms)
 // XT: element type of the source x (and of PRE's y): bf16 for C4's fused-chain activations / gradients
 template <int NT, int WT, class EP, bool XCD_REMAP, int ABL = (NT >= 6 ? 0 : 1), class PRE = PreNone, class XT = float>
 __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo_x3_kernel(const XT* __restrict__ x, int H, int Cin,
@@ -1835,7 +1837,11 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
     if constexpr (TALL)
         ep.tall(acc, t * HB + wm * 128, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(Hs + (hb ^ 1) * NS * HPLANE),
                 tid);
-    else
+    else if constexpr (ABL & 16384) {   // timing ablation: the epilogue skipped (kept live behind a never-taken branch)
+        if (acc[0][0][0] == 1.2345e-30f)
+            ep(acc, t * HB + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(Hs + (hb ^ 1) * NS * HPLANE),
+               tid);
+    } else
         ep(acc, t * HB + wm * 64, n0 + wn * 64, lane, wm, wn, reinterpret_cast<float*>(Hs + (hb ^ 1) * NS * HPLANE), tid);
     if (nextt) __syncthreads();
     }
