@@ -206,6 +206,24 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
     int ymm_ld = 0;              //   ymm[n] (atomic max), ymm[ymm_ld + n] (atomic min); needs stats
     EpiFuse fz{};                // FUSE: the eval-mode output transform (LDS-halo conv, whole 256-pixel tiles)
 
+    // Addresses of a wave tile's 64 accumulator elements (i, j, r) — row mw + 32 i + (r & 3) + 8 (r >> 2) + 4 (lane >> 5),
+    // column nw + 32 j + (lane & 31) — as a wave-uniform base (scalar arithmetic: mw / nw are wave-uniform, made so for
+    // the compiler by readfirstlane) plus ONE lane byte offset shared by all 64 of them.  Written as y + (long long)m *
+    // ldy + n per element, every address cost two v_mul_lo_u32 and a v_mad_u64_u32 (quarter-rate VALU) — the bulk of
+    // the epilogue's issue time, which no MFMA overlaps (round 6).
+    struct WaveAddr {
+        OT* base; long long ldy; unsigned lb;
+        __device__ __forceinline__ OT* at(int i, int j, int r) const {
+            return reinterpret_cast<OT*>(reinterpret_cast<char*>(base + (long long)(32 * i + (r & 3) + 8 * (r >> 2)) * ldy
+                                                                 + 32 * j) + lb);
+        }
+    };
+    __device__ __forceinline__ WaveAddr wave_addr(OT* yb, int mw, int nw, int lane) const {
+        const int mu = __builtin_amdgcn_readfirstlane(mw), nu = __builtin_amdgcn_readfirstlane(nw);
+        return WaveAddr{yb + (long long)mu * ldy + nu, ldy,
+                        (unsigned)(4 * (lane >> 5) * (int)ldy + (lane & 31)) * (unsigned)sizeof(OT)};
+    }
+
     // FUSE (eval forward, conv3x3_halo_x3_kernel): relu(acc + bias), then fz's transform; the whole block tile is in
     // range (host: M % 256 == 0, N % 128 == 0) and a 256-pixel tile lies in one image (hw % 256 == 0).  POOL: at
     // W = 32 a wave's two row blocks are two image rows (the 2x2 window is in registers); at W = 64 a wave holds one
@@ -281,18 +299,22 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
                 cb[j] = resid ? fz.b[sel + n] : fz.fb[img * fz.fbn + n];
             }
             if (resid) {
+                const float* xb = fz.x + __builtin_amdgcn_readfirstlane(mw);
+                const unsigned lx = (unsigned)(4 * (lane >> 5)) * 4u;
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
                     for (int r = 0; r < 16; ++r)
-                        xv[i][r] = fz.x[mw + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
+                        xv[i][r] = *reinterpret_cast<const float*>(
+                            reinterpret_cast<const char*>(xb + 32 * i + (r & 3) + 8 * (r >> 2)) + lx);
             }
+            const WaveAddr wa = wave_addr(y, mw, nw, lane);
             CDM_FOR_ACC({
                 float v = relu_f(acc[i][j][r] + bj[j]);
                 if (resid) v = fmaf(ca[j], xv[i][r], cb[j]) + v;
                 else v = fmaf(ca[j], v, cb[j]);
                 v = Act<OT>::round(v);
-                Act<OT>::store(y + (long long)m * ldy + n, v);
+                Act<OT>::store(wa.at(i, j, r), v);
                 am = fmaxf(am, fabsf(v));
             })
         }
@@ -317,6 +339,7 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
             for (int j = 0; j < 2; ++j) bj[j] = bias ? bias[(nw + 32 * j + (lane & 31)) % bias_mod] : 0.f;
             const bool relu = flags & EPI_RELU;
             const bool accum = flags & EPI_ACCUM;
+            const WaveAddr wa = wave_addr(yz, mw, nw, lane);
             if constexpr (ACC) {
                 // accumulate (a compile-time variant: the interleaved form below waited on one load per element — the
                 // compiler cannot prove the addresses disjoint — +0.5 ms per accumulating 64^2 dgrad, profiles/
@@ -328,34 +351,39 @@ struct EpiStoreW {  // y[m*ldy + n] (+)= acc + bias[n % bias_mod]; optional per-
                     for (int j = 0; j < 2; ++j) {
                         float old[16];
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            const int m = mw + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                            old[r] = Act<OT>::load(yz + (long long)m * ldy + nw + 32 * j + (lane & 31));
-                        }
+                        for (int r = 0; r < 16; ++r) old[r] = Act<OT>::load(wa.at(i, j, r));
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
-                            const int m = mw + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                            const int n = nw + 32 * j + (lane & 31);
                             float v = acc[i][j][r] + bj[j] + old[r];
                             if (relu) v = relu_f(v);
                             v = Act<OT>::round(v);
-                            Act<OT>::store(yz + (long long)m * ldy + n, v);
+                            Act<OT>::store(wa.at(i, j, r), v);
                             cs[j] += v; cq[j] += v * v;
                             am = fmaxf(am, fabsf(v));
                             cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
                         }
                     }
             } else {
-                CDM_FOR_ACC({
-                    float v = acc[i][j][r] + bj[j];
-                    if (accum) v += Act<OT>::load(yz + (long long)m * ldy + n);
-                    if (relu) v = relu_f(v);
-                    v = Act<OT>::round(v);
-                    Act<OT>::store(yz + (long long)m * ldy + n, v);
-                    cs[j] += v; cq[j] += v * v;
-                    am = fmaxf(am, fabsf(v));
-                    cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
-                })
+                // the runtime accumulate flag hoisted out of the 64 elements (a uniform branch per element split the
+                // epilogue into 64 basic blocks, each with its own vmcnt(0) wait)
+                // (and the column statistics, when the launch records none: the eval forwards)
+                auto body = [&](auto accum_tag, auto stats_tag) {
+                    CDM_FOR_ACC({
+                        float v = acc[i][j][r] + bj[j];
+                        if constexpr (decltype(accum_tag)::value) v += Act<OT>::load(wa.at(i, j, r));
+                        if (relu) v = relu_f(v);
+                        v = Act<OT>::round(v);
+                        Act<OT>::store(wa.at(i, j, r), v);
+                        am = fmaxf(am, fabsf(v));
+                        if constexpr (decltype(stats_tag)::value) {
+                            cs[j] += v; cq[j] += v * v;
+                            cmx[j] = fmaxf(cmx[j], v); cmn[j] = fminf(cmn[j], v);
+                        }
+                    })
+                };
+                if (accum) body(std::true_type{}, std::true_type{});
+                else if (stats) body(std::false_type{}, std::true_type{});
+                else body(std::false_type{}, std::false_type{});
             }
         } else {
             CDM_FOR_ACC({
@@ -569,6 +597,33 @@ struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n,
             const int ij = nok[j] ? n / Co : 0, co = nok[j] ? n - ij * Co : 0;
             coff[j] = ((long long)(ij >> 1) * (2 * W) + (ij & 1)) * ldy + co;
             bj[j] = bias ? bias[co] : 0.f;
+        }
+        if ((W == 16 || W % 32 == 0) && hw % 32 == 0 && mw + 64 <= M && nw + 64 <= N) {
+            // (round 6) the wave's two 32-pixel row blocks each lie in one image and span at most two input rows (W =
+            // 16: rows d < 16 and d >= 16; W >= 32: one row), so element r of a lane is its row block's first pixel
+            // plus a wave-uniform output offset: one 64-bit lane pointer per row block, scalar offsets per element
+            // (the carry walk below formed a 64-bit index product per element)
+            const int mu = __builtin_amdgcn_readfirstlane(mw);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int mb = mu + 32 * i + 4 * (lane >> 5);
+                const int b = mb / hw, rem = mb - b * hw, h = rem / W, w = rem - h * W;
+                const float* pl0 = y + ((long long)(b * 2 * H + 2 * h) * (2 * W) + 2 * w) * ldy;
+                float* pl = const_cast<float*>(pl0);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int d = (r & 3) + 8 * (r >> 2);
+                    const long long dd = (W >= 32 || d < 16) ? 2 * d : 4 * W + 2 * (d - 16);   // output pixels
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const float v = acc[i][j][r] + bj[j];
+                        pl[dd * ldy + coff[j]] = v;
+                        am = fmaxf(am, fabsf(v));
+                    }
+                }
+            }
+            if (amax) block_amax_commit(am, amax);
+            return;
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -1343,7 +1398,10 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
                                                                       int ldx, const __bf16* __restrict__ wx3,
                                                                       int Cout, const float* amax_x,
                                                                       const float* amax_w, EP ep, PRE pre,
-                                                                      int mtiles, int tpb, int stg = 0) {
+                                                                      int mtiles, int tpb, int stgd = 0) {
+    // stgd: bit 0 the staggered halo split (halo_stagger); bits 8+: the start delay of every other block in 10 ns
+    // ticks (halo_delay: desynchronises the blocks' epilogue store bursts)
+    const int stg = stgd & 255;
     constexpr int NS = XTerms<NT>::NS;
     // TALL (ABL 8192, one bf16 term only): 4 waves (one per SIMD, 512 registers each: the accumulators live in AGPRs) as
     // 2 (M) x 2 (N) of 128 x 64 — 4 row blocks of 32 pixels per wave.  The one-term MFMA reads 1 KiB of fragments per
@@ -1398,6 +1456,13 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
         t_step = cnt;
     }
     if (t_first >= mtiles) return;   // cannot happen for grid.x = ceil(mtiles / tpb); uniform per block
+    if (const unsigned dly = (unsigned)stgd >> 8; dly && ((blockIdx.x >> 3) & 1)) {
+        // every other block of each XCD starts dly x 10 ns late (s_memrealtime: 100 MHz), so that half the CUs store
+        // their tile's y while the other half compute (all blocks otherwise reach every epilogue together and the
+        // chip's write bandwidth, not the MFMAs, paces those microseconds)
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < dly) __builtin_amdgcn_s_sleep(4);
+    }
     const int n0 = blockIdx.y * GBN;
     const int hw = H * WT;
     const int nchunks = Cin / 16, ngroups = nchunks * 3;
@@ -2308,16 +2373,20 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
     float ia = 1.f, ib = 1.f;
     if constexpr (NT == NT_H3) { ia = 1.f / sa; ib = 1.f / sb; }
     const int NN = 9 * Cin;
-    float* sz = slab + (long long)bz * Cout * NN;
+    // wave-uniform base + one lane byte offset for all 96 stores (per-element 64-bit index products were quarter-rate
+    // VALU; see EpiStoreW::WaveAddr)
+    float* sz = slab + (long long)bz * Cout * NN + (long long)(m0 + __builtin_amdgcn_readfirstlane(wm) * 64) * NN
+              + ky * 3 * Cin + ci0 + __builtin_amdgcn_readfirstlane(wn) * 32;
+    const unsigned lb = (unsigned)(4 * (lane >> 5) * NN + (lane & 31)) * 4u;
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
-        const int n = (ky * 3 + t) * Cin + ci0 + wn * 32 + (lane & 31);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                sz[(long long)m * NN + n] = NT == NT_H3 ? (acc[t][i][r] * ia) * ib : acc[t][i][r];
+                float* p = sz + (long long)(32 * i + (r & 3) + 8 * (r >> 2)) * NN + t * Cin;
+                *reinterpret_cast<float*>(reinterpret_cast<char*>(p) + lb) =
+                    NT == NT_H3 ? (acc[t][i][r] * ia) * ib : acc[t][i][r];
             }
     }
 }
@@ -2345,7 +2414,9 @@ static int halo_tpb(int mtiles, int ntiles, int nterm, int wt) {
 // ms; C4 (bf16) 32.20-32.21 -> 32.26-32.40 ms (its halo split is a plain conversion: nothing left to hide)
 static int halo_stagger(int nterm) {   // default on for h3 and (round 4, profiles/r4_ab_c4_knobs.txt) for bf16
     static const int v = [] { const char* e = getenv("CDM_HALO_STAGGER"); return e ? atoi(e) : -1; }();
-    return v >= 0 ? v : ((nterm == NT_H3 || nterm == 1) ? 1 : 0);
+    // + the block start delay (bits 8+, 10 ns ticks; $CDM_HALO_DELAY)
+    static const int d = [] { const char* e = getenv("CDM_HALO_DELAY"); return e ? atoi(e) : 0; }();
+    return (v >= 0 ? v : ((nterm == NT_H3 || nterm == 1) ? 1 : 0)) | (d << 8);
 }
 
 // the one-barrier-per-chunk schedule of the one-term (bf16) LDS-halo conv ($CDM_HALO_ONEB=0: three barriers per chunk)
