@@ -22,9 +22,20 @@ static __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_ca
 // conversion does not force a wait at the load site); to4() widens it (bf16 -> fp32 is exact); round() is the value a
 // store of v keeps.
 template <class T> struct Act;
+// raw buffer resource over [base, base + 2^31 - 16): a load at byte offset BUF_OOB or beyond returns zeros (the range
+// check of a stride-0 buffer), which turns a masked / padded load into an unconditional one with a selected offset
+constexpr unsigned BUF_OOB = 0x80000000u;
+static __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7FFFFFF0, 0x00020000);
+}
 template <> struct Act<float> {
     typedef float4 Raw;
     static __device__ __forceinline__ Raw load4(const void* p) { return *reinterpret_cast<const float4*>(p); }
+    static __device__ __forceinline__ Raw bload4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+    }
     static __device__ __forceinline__ float4 to4(const Raw& r) { return r; }
     static __device__ __forceinline__ Raw zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
     static __device__ __forceinline__ float round(float v) { return v; }
@@ -34,6 +45,11 @@ template <> struct Act<float> {
 template <> struct Act<__bf16> {
     typedef uint2 Raw;
     static __device__ __forceinline__ Raw load4(const void* p) { return *reinterpret_cast<const uint2*>(p); }
+    static __device__ __forceinline__ Raw bload4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        const u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        return make_uint2(v.x, v.y);
+    }
     static __device__ __forceinline__ float4 to4(const Raw& r) {
         return make_float4(__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u), __uint_as_float(r.y << 16),
                            __uint_as_float(r.y & 0xffff0000u));

@@ -2168,6 +2168,26 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
             cf[k][0] = v.x; cf[k][1] = v.y; cf[k][2] = v.z; cf[k][3] = v.w;
         }
     }
+    // K-step loads as buffer loads: the step's pixel (pn, ph, pw) is wave-uniform, so each operand's address is a
+    // uniform base (scalar arithmetic, a new resource per step) + a per-lane byte offset that is the same for every step
+    // (pixel sr + 16 k of the step, channel quad c4); padding pieces (outside the image, and the sums' skipped pieces)
+    // take offset BUF_OOB and read zeros.  Round 6: the per-load 64-bit index products (two v_mul_lo_u32 and a
+    // v_mad_u64_u32, quarter-rate) and the exec-masked zero fills were the bulk of this VALU-issue-bound loop's non-MFMA
+    // instructions.
+    // (two-term h3 only: for the one-term bf16 kernels it measured slower, 26.53 -> 26.99 ms per C4 step; C2 48.61 ->
+    // 48.42 ms, profiles/r6_ab_wgrad_bufld.txt)
+    constexpr bool BUFLD = NT == NT_H3;
+    unsigned odg[KS], ody[KS], oxk[KS], ogk[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+        odg[k] = (unsigned)((sr + 16 * k) * lddy + c4) * (unsigned)sizeof(GT);
+        if constexpr (PRE::on) ody[k] = (unsigned)((sr + 16 * k) * pre.ldy + c4) * (unsigned)sizeof(GT);
+        oxk[k] = (unsigned)((sr + 16 * k) * ldx + c4) * (unsigned)sizeof(XT);
+        if constexpr (SUMS) ogk[k] = (unsigned)((sr + 16 * k) * px.ldg + c4) * (unsigned)sizeof(XT);
+    }
+    const unsigned ox1 = (unsigned)((RA + sr) * ldx + c4) * (unsigned)sizeof(XT);
+    unsigned og1 = 0u;
+    if constexpr (SUMS) og1 = (unsigned)((RA + sr) * px.ldg + c4) * (unsigned)sizeof(XT);
     auto gload = [&]() {   // the K step at (pn, ph, pw), then advance by RA pixels
         const int hh = ph + ky - 1;
         const bool rowok = (unsigned)hh < (unsigned)H;
@@ -2177,51 +2197,87 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
             const long long q = ((long long)(pn * H + ph) * W + pw) / RA;
             sum_step = rowok && ky == ks && (int)(q % gx) == (m0 >> 7);
         }
-#pragma unroll
-        for (int k = 0; k < KS; ++k) {
-            const long long pix = (long long)(pn * H + ph) * W + pw + sr + 16 * k;
-            ra[k] = Act<GT>::load4(dy + pix * lddy + m0 + c4);
-            if constexpr (PRE::on) ya[k] = Act<GT>::load4(reinterpret_cast<const GT*>(pre.y) + pix * pre.ldy + m0 + c4);
-            const int w0 = pw - 1 + sr + 16 * k;
-            vb[k] = rowok && (unsigned)w0 < (unsigned)W;
-            rb[k] = vb[k] ? Act<XT>::load4(x + (xrow + w0) * ldx + ci0 + c4) : Act<XT>::zero();
-            if constexpr (SUMS) {   // central rows 1..RA of the X image (the step's own columns, inside the image)
-                gr[k] = (sum_step && (k > 0 || sr >= 1))
-                            ? Act<XT>::load4(reinterpret_cast<const XT*>(px.g) + (xrow + w0) * px.ldg + ci0 + c4)
-                            : Act<XT>::zero();
+        if constexpr (BUFLD) {
+            const long long pix0 = (long long)(pn * H + ph) * W + pw;            // the step's first output pixel
+            const long long xp0 = xrow + pw - 1;                                 // its X image's first pixel (halo)
+            const auto rdy = buf_rsrc(dy + pix0 * lddy + m0);
+            const auto rx = buf_rsrc(x + xp0 * ldx + ci0);
+    #pragma unroll
+            for (int k = 0; k < KS; ++k) {
+                ra[k] = Act<GT>::bload4(rdy, odg[k]);
+                if constexpr (PRE::on)
+                    ya[k] = Act<GT>::bload4(buf_rsrc(reinterpret_cast<const GT*>(pre.y) + pix0 * pre.ldy + m0), ody[k]);
+                const int w0 = pw - 1 + sr + 16 * k;
+                vb[k] = rowok && (unsigned)w0 < (unsigned)W;
+                rb[k] = Act<XT>::bload4(rx, vb[k] ? oxk[k] : BUF_OOB);
+                if constexpr (SUMS) {   // central rows 1..RA of the X image (the step's own columns, inside the image)
+                    const auto rg = buf_rsrc(reinterpret_cast<const XT*>(px.g) + xp0 * px.ldg + ci0);
+                    gr[k] = Act<XT>::bload4(rg, (sum_step && (k > 0 || sr >= 1)) ? ogk[k] : BUF_OOB);
+                }
             }
-        }
-        if (tid < 64) {
-            const int w1 = pw + RA - 1 + sr;
-            vb1 = rowok && w1 < W;
-            rb1 = vb1 ? Act<XT>::load4(x + (xrow + w1) * ldx + ci0 + c4) : Act<XT>::zero();
-            if constexpr (SUMS)
-                gr1 = (sum_step && tid < 32)
-                          ? Act<XT>::load4(reinterpret_cast<const XT*>(px.g) + (xrow + w1) * px.ldg + ci0 + c4)
-                          : Act<XT>::zero();
+            if (tid < 64) {   // (wave 0: a uniform branch)
+                const int w1 = pw + RA - 1 + sr;
+                vb1 = rowok && w1 < W;
+                rb1 = Act<XT>::bload4(rx, vb1 ? ox1 : BUF_OOB);
+                if constexpr (SUMS) {
+                    const auto rg = buf_rsrc(reinterpret_cast<const XT*>(px.g) + xp0 * px.ldg + ci0);
+                    gr1 = Act<XT>::bload4(rg, (sum_step && tid < 32) ? og1 : BUF_OOB);
+                }
+            }
+        } else {   // one-term (C4): plain loads (the buffer form measured 26.53 -> 26.99 ms per C4 step)
+    #pragma unroll
+            for (int k = 0; k < KS; ++k) {
+                const long long pix = (long long)(pn * H + ph) * W + pw + sr + 16 * k;
+                ra[k] = Act<GT>::load4(dy + pix * lddy + m0 + c4);
+                if constexpr (PRE::on) ya[k] = Act<GT>::load4(reinterpret_cast<const GT*>(pre.y) + pix * pre.ldy + m0 + c4);
+                const int w0 = pw - 1 + sr + 16 * k;
+                vb[k] = rowok && (unsigned)w0 < (unsigned)W;
+                rb[k] = vb[k] ? Act<XT>::load4(x + (xrow + w0) * ldx + ci0 + c4) : Act<XT>::zero();
+                if constexpr (SUMS) {   // central rows 1..RA of the X image (the step's own columns, inside the image)
+                    gr[k] = (sum_step && (k > 0 || sr >= 1))
+                                ? Act<XT>::load4(reinterpret_cast<const XT*>(px.g) + (xrow + w0) * px.ldg + ci0 + c4)
+                                : Act<XT>::zero();
+                }
+            }
+            if (tid < 64) {
+                const int w1 = pw + RA - 1 + sr;
+                vb1 = rowok && w1 < W;
+                rb1 = vb1 ? Act<XT>::load4(x + (xrow + w1) * ldx + ci0 + c4) : Act<XT>::zero();
+                if constexpr (SUMS)
+                    gr1 = (sum_step && tid < 32)
+                              ? Act<XT>::load4(reinterpret_cast<const XT*>(px.g) + (xrow + w1) * px.ldg + ci0 + c4)
+                              : Act<XT>::zero();
+            }
         }
         pw += RA;
         if (pw >= W) { pw = 0; if (++ph == H) { ph = 0; ++pn; } }
     };
-    auto xsum = [&](const float4& v, const float4& gv) {     // PreBnReluSums: one central piece
+    // (lane conditions as selects, not branches: a divergent `if` around a piece cost an exec save / restore and four
+    // register copies per piece; the pieces a condition drops were loaded as zeros, BUF_OOB)
+    auto xsum = [&](const float4& v, const float4& gv, bool on) {     // PreBnReluSums: one central piece
         if constexpr (SUMS) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const float y = f4get(v, e);
                 const float zp = fmaf(y, xs[e], xt[e]);
                 const float xh = (y - xm[e]) * xi[e];
-                const float gp = zp > 0.f ? f4get(gv, e) : 0.f;
-                s1[e] += gp; s2[e] += gp * xh; s5[e] += xh;
+                const float gp = zp > 0.f ? f4get(gv, e) : 0.f;   // (g is 0 where !on: nothing to mask in s1, s2)
+                s1[e] += gp; s2[e] += gp * xh; s5[e] += on ? xh : 0.f;
             }
         }
     };
     auto xpre = [&](const float4& v, bool valid) -> float4 {   // PX transform at staging time (after the load wait)
         if constexpr (PX::kind >= 2) {
-            if (valid)
+            if constexpr (BUFLD)
+                return make_float4(valid ? bn_relu_elem(v.x, xs[0], xt[0]) : 0.f,
+                                   valid ? bn_relu_elem(v.y, xs[1], xt[1]) : 0.f,
+                                   valid ? bn_relu_elem(v.z, xs[2], xt[2]) : 0.f,
+                                   valid ? bn_relu_elem(v.w, xs[3], xt[3]) : 0.f);
+            else if (valid)
                 return make_float4(bn_relu_elem(v.x, xs[0], xt[0]), bn_relu_elem(v.y, xs[1], xt[1]),
                                    bn_relu_elem(v.z, xs[2], xt[2]), bn_relu_elem(v.w, xs[3], xt[3]));
         }
-        return v;
+        return v;   // (padding pieces were loaded as zeros)
     };
     auto put = [&](char* img, int row, const float4& v, float sc, int ielems) {
         const float xv[4] = {v.x, v.y, v.z, v.w};
@@ -2258,7 +2314,12 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
             } else {
                 const float4 xk = Act<XT>::to4(rb[k]);
                 if constexpr (SUMS) {
-                    if (sum_step && (k > 0 || sr >= 1)) xsum(xk, Act<XT>::to4(gr[k]));
+                    // (sum_step: block-uniform; the lane condition sr >= 1 only splits wave 0 at k = 0)
+                    if constexpr (BUFLD) {
+                        if (sum_step) xsum(xk, Act<XT>::to4(gr[k]), k > 0 || sr >= 1);
+                    } else {
+                        if (sum_step && (k > 0 || sr >= 1)) xsum(xk, Act<XT>::to4(gr[k]), true);
+                    }
                 }
                 put(b, sr + 16 * k, xpre(xk, vb[k]), sb, IB);
             }
@@ -2268,7 +2329,11 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
         } else {
             const float4 x1 = Act<XT>::to4(rb1);
             if constexpr (SUMS) {
-                if (sum_step && tid < 32) xsum(x1, Act<XT>::to4(gr1));
+                if constexpr (BUFLD) {
+                    if (sum_step && tid < 64) xsum(x1, Act<XT>::to4(gr1), tid < 32);   // (wave 0 only: uniform)
+                } else {
+                    if (sum_step && tid < 32) xsum(x1, Act<XT>::to4(gr1), true);
+                }
             }
             if (tid < 64) put(b, RA + sr, xpre(x1, vb1), sb, IB);
         }
