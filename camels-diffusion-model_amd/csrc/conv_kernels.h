@@ -2255,6 +2255,9 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
     // (lane conditions as selects, not branches: a divergent `if` around a piece cost an exec save / restore and four
     // register copies per piece; the pieces a condition drops were loaded as zeros, BUF_OOB)
     auto xsum = [&](const float4& v, const float4& gv, bool on) {     // PreBnReluSums: one central piece
+        // (contraction off, the fused products spelled out: the compiler's free fmul + fadd fusion decided differently
+        // in the two inlined copies of the staging (the wave schedules), so the sums' last bits depended on the schedule)
+#pragma clang fp contract(off)
         if constexpr (SUMS) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -2262,7 +2265,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
                 const float zp = fmaf(y, xs[e], xt[e]);
                 const float xh = (y - xm[e]) * xi[e];
                 const float gp = zp > 0.f ? f4get(gv, e) : 0.f;   // (g is 0 where !on: nothing to mask in s1, s2)
-                s1[e] += gp; s2[e] += gp * xh; s5[e] += on ? xh : 0.f;
+                s1[e] += gp; s2[e] = fmaf(gp, xh, s2[e]); s5[e] += on ? xh : 0.f;
             }
         }
     };
@@ -2396,20 +2399,25 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
         }
         }
     };
+    // stg: the two waves of each SIMD (w, w + 4) run the step in opposite orders — one stages the next K step
+    // (VALU: BN transforms, term split, LDS writes) while the other issues its MFMAs, instead of both alternating in
+    // lock-step between the barriers.  The staging-first wave loads one K step further ahead (its registers are free
+    // once it has staged), so its staging finds the data in flight since the previous step's MFMAs (round 3's form
+    // loaded at the top of the step and waited out the whole HBM latency there).
+    const bool early = stg && wave >= 4;
     if (kt0 < kt1) { gload(); sstore(smem); }
+    if (early && kt0 + 1 < kt1) gload();
     __syncthreads();
     int cur = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = kt + 1 < kt1;
-        if (more) gload();
         auto mma = [&]() { mma_at(cur); };
-        // stg: the two waves of each SIMD (w, w + 4) run the step in opposite orders — one stages the next K step
-        // (VALU: BN transforms, term split, LDS writes) while the other issues its MFMAs, instead of both
-        // alternating in lock-step between the barriers
-        if (stg && wave >= 4) {
+        if (early) {
             if (more) sstore(smem + (cur ^ 1) * STEP);
+            if (kt + 2 < kt1) gload();
             mma();
         } else {
+            if (more) gload();
             mma();
             if (more) sstore(smem + (cur ^ 1) * STEP);
         }
