@@ -1399,9 +1399,10 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
                                                                       int Cout, const float* amax_x,
                                                                       const float* amax_w, EP ep, PRE pre,
                                                                       int mtiles, int tpb, int stgd = 0) {
-    // stgd: bit 0 the staggered halo split (halo_stagger); bits 8+: the start delay of every other block in 10 ns
+    // stgd: bit 0 the staggered halo split (halo_stagger), bit 1 waves 4-7 at priority 1; bits 8+: the start delay of
+    // every other block in 10 ns
     // ticks (halo_delay: desynchronises the blocks' epilogue store bursts)
-    const int stg = stgd & 255;
+    const int stg = stgd & 1;
     constexpr int NS = XTerms<NT>::NS;
     // TALL (ABL 8192, one bf16 term only): 4 waves (one per SIMD, 512 registers each: the accumulators live in AGPRs) as
     // 2 (M) x 2 (N) of 128 x 64 — 4 row blocks of 32 pixels per wave.  The one-term MFMA reads 1 KiB of fragments per
@@ -1439,7 +1440,7 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    if constexpr (ABL & 512) {
+    if ((ABL & 512) || (stgd & 2)) {   // static priority for the second-dispatched half (stgd bit 1: $CDM_HALO_PRIO)
         if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     }
     // the block's tpb 256-pixel tiles, run one after the other: the next tile's first halo and B are fetched
@@ -2404,7 +2405,8 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
     // lock-step between the barriers.  The staging-first wave loads one K step further ahead (its registers are free
     // once it has staged), so its staging finds the data in flight since the previous step's MFMAs (round 3's form
     // loaded at the top of the step and waited out the whole HBM latency there).
-    const bool early = stg && wave >= 4;
+    const bool early = (stg & 1) && wave >= 4;
+    if ((stg & 2) && wave >= 4) __builtin_amdgcn_s_setprio(1);   // stg bit 1: the staging-first half at priority 1
     if (kt0 < kt1) { gload(); sstore(smem); }
     if (early && kt0 + 1 < kt1) gload();
     __syncthreads();
@@ -2489,7 +2491,9 @@ static int halo_stagger(int nterm) {   // default on for h3 and (round 4, profil
     static const int v = [] { const char* e = getenv("CDM_HALO_STAGGER"); return e ? atoi(e) : -1; }();
     // + the block start delay (bits 8+, 10 ns ticks; $CDM_HALO_DELAY)
     static const int d = [] { const char* e = getenv("CDM_HALO_DELAY"); return e ? atoi(e) : 0; }();
-    return (v >= 0 ? v : ((nterm == NT_H3 || nterm == 1) ? 1 : 0)) | (d << 8);
+    // + static priority 1 for waves 4-7 (bit 1; $CDM_HALO_PRIO)
+    static const int p = [] { const char* e = getenv("CDM_HALO_PRIO"); return e ? atoi(e) : 0; }();
+    return (v >= 0 ? v : ((nterm == NT_H3 || nterm == 1) ? 1 : 0)) | (p ? 2 : 0) | (d << 8);
 }
 
 // the one-barrier-per-chunk schedule of the one-term (bf16) LDS-halo conv ($CDM_HALO_ONEB=0: three barriers per chunk)
