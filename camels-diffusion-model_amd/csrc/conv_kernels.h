@@ -2410,8 +2410,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
     // loaded at the top of the step and waited out the whole HBM latency there).
     const bool early = (stg & 1) && wave >= 4;
     if ((stg & 2) && wave >= 4) __builtin_amdgcn_s_setprio(1);   // stg bit 1: the staging-first half at priority 1
+    // stg bit 2: the MFMA-first half also loads the step after next once it has staged (before the barrier, not after)
+    const bool ahead = early || (stg & 4);
     if (kt0 < kt1) { gload(); sstore(smem); }
-    if (early && kt0 + 1 < kt1) gload();
+    if (ahead && kt0 + 1 < kt1) gload();
     __syncthreads();
     int cur = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
@@ -2421,6 +2423,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
             if (more) sstore(smem + (cur ^ 1) * STEP);
             if (kt + 2 < kt1) gload();
             mma();
+        } else if (ahead) {
+            mma();
+            if (more) sstore(smem + (cur ^ 1) * STEP);
+            if (kt + 2 < kt1) gload();
         } else {
             if (more) gload();
             mma();

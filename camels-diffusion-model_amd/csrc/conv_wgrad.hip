@@ -1,17 +1,20 @@
 // conv3x3 weight gradient (kernel-row and transposed-read kernels, split-GEMM fallback): C ABI.  Kernels: conv_kernels.h.
 #include "conv_kernels.h"
 
-// the staggered wave order of the kernel-row weight gradient ($CDM_WGRAD_STAGGER, default 1 since round 6).  Round 3's
+// the staggered wave order of the kernel-row weight gradient ($CDM_WGRAD_STAGGER, default 5 since round 6).  Round 3's
 // form was slower (C2 train step 52.11-52.42 -> 52.88-53.05 ms, C4 32.26-32.52 -> 33.38-33.61 ms, profiles/
 // r3_ab_wgrad_stagger.txt): the staging-first wave waited on the K step's loads it had just issued.  Round 6: that wave
 // loads one K step further ahead — same-box A/B, 3 rounds, C2 48.10-48.16 -> 47.02-47.09 ms and C4 25.63-25.68 ->
-// 25.24-25.27 ms per train step, slabs and sums bit-identical (profiles/r6_ab_wgrad_stagger_early.txt)
+// 25.24-25.27 ms per train step, slabs and sums bit-identical (profiles/r6_ab_wgrad_stagger_early.txt).  Bit 2 (default
+// value 5 = 1 | 4): the MFMA-first half, too, loads the step after next once it has staged (before the barrier rather
+// than after it): C2 46.75-46.77 -> 46.16-46.26 ms, C4 neutral (25.24-26.05 -> 25.44-25.71), bit-identical
+// (profiles/r6_ab_wgrad_ahead.txt)
 static int wgrad_ks4() {
     static const int v = [] { const char* e = getenv("CDM_WGRAD_KS4"); return e ? atoi(e) : 1; }();
     return v;
 }
 static int wgrad_stagger() {
-    static const int v = [] { const char* e = getenv("CDM_WGRAD_STAGGER"); return e ? atoi(e) : 1; }();
+    static const int v = [] { const char* e = getenv("CDM_WGRAD_STAGGER"); return e ? atoi(e) : 5; }();
     return v;
 }
 
