@@ -1981,8 +1981,11 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
     // running image coordinates of the K step's first pixel
     int p0 = kt0 * 16;
     int pn = p0 / hw, ph = (p0 - pn * hw) / W, pw = p0 - pn * hw - ph * W;
-    float4 ra[KS][2], rb[KS][2];
-    auto gload = [&](int kt) {          // the KS K steps from kt (zero past kt1)
+    // DEEP2 (CT, KS = 1; round 6): two register sets, the K step two ahead in flight while one computes — a ConvT K step
+    // is 12 MFMAs per wave, far too short to cover the HBM latency of loads issued one step ahead
+    constexpr bool DEEP2 = CT && KS == 1;
+    float4 ra[KS][2], rb[KS][2], ra2[DEEP2 ? KS : 1][2], rb2[DEEP2 ? KS : 1][2];
+    auto gload_to = [&](float4 (&ra)[KS][2], float4 (&rb)[KS][2], int kt) {   // the KS K steps from kt (zero past kt1)
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const bool ok = kt + ks < kt1;
@@ -2005,7 +2008,8 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
             if (pw >= W) { pw = 0; if (++ph == H) { ph = 0; ++pn; } }
         }
     };
-    auto sstore = [&](__bf16* base0) {
+    auto gload = [&](int kt) { gload_to(ra, rb, kt); };
+    auto sstore_from = [&](const float4 (&ra)[KS][2], const float4 (&rb)[KS][2], __bf16* base0) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -2023,6 +2027,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
                 for (int k = 0; k < NS; ++k) *reinterpret_cast<u32x2*>(d + k * IMG * 2) = tm[k];
             }
     };
+    auto sstore = [&](__bf16* base0) { sstore_from(ra, rb, base0); };
     // transposed-read addresses: lane 4q+p of 16-lane group g supplies row kb+q, columns c0+4p..+3
     const int g = (lane >> 4) & 3, q = (lane >> 2) & 3, pq = lane & 3;
     const int kb = 8 * (g >> 1) + q;
@@ -2037,12 +2042,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
         }
     }
 
-    if (kt0 < kt1) { gload(kt0); sstore(smem); }
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kt0; kt < kt1; kt += KS) {
-        const bool more = kt + KS < kt1;
-        if (more) gload(kt + KS);
+    auto mma_at = [&](int cur) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
         const char* a = reinterpret_cast<const char*>(smem + (cur * KS + ks) * STEP);
@@ -2076,9 +2076,37 @@ __global__ __launch_bounds__(GTHREADS, 2) void wgrad3x3_tr_x3_kernel(const float
                 acc[i][j] = xmfma<NT>(fa[i][0], fb[j][0], c);
             }
         }
-        if (more) sstore(smem + (cur ^ 1) * KS * STEP);
+    };
+    if constexpr (DEEP2) {
+        if (kt0 < kt1) { gload_to(ra, rb, kt0); sstore_from(ra, rb, smem); }
+        if (kt0 + 1 < kt1) gload_to(ra2, rb2, kt0 + 1);
         __syncthreads();
-        cur ^= 1;
+        int cur = 0;
+        for (int kt = kt0; kt < kt1; kt += 2) {   // set (ra, rb): even steps, (ra2, rb2): odd steps
+            if (kt + 2 < kt1) gload_to(ra, rb, kt + 2);
+            mma_at(cur);
+            if (kt + 1 < kt1) sstore_from(ra2, rb2, smem + (cur ^ 1) * STEP);
+            __syncthreads();
+            cur ^= 1;
+            if (kt + 1 >= kt1) break;
+            if (kt + 3 < kt1) gload_to(ra2, rb2, kt + 3);
+            mma_at(cur);
+            if (kt + 2 < kt1) sstore_from(ra, rb, smem + (cur ^ 1) * STEP);
+            __syncthreads();
+            cur ^= 1;
+        }
+    } else {
+        if (kt0 < kt1) { gload(kt0); sstore(smem); }
+        __syncthreads();
+        int cur = 0;
+        for (int kt = kt0; kt < kt1; kt += KS) {
+            const bool more = kt + KS < kt1;
+            if (more) gload(kt + KS);
+            mma_at(cur);
+            if (more) sstore(smem + (cur ^ 1) * KS * STEP);
+            __syncthreads();
+            cur ^= 1;
+        }
     }
     unscale<NT>(acc, sdy_, sx_);
     EpiStore e = ep;                       // this block's split slab (the epilogue would index blockIdx.z)
