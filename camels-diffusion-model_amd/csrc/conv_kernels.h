@@ -2141,7 +2141,13 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
     // (one bf16 term with 16-pixel K steps stages only 8704)
     constexpr int SMEM = (PX::kind == 3 && 2 * STEP < 2 * 16 * 3 * 128) ? 2 * 16 * 3 * 128 : 2 * STEP;
     __shared__ __attribute__((aligned(16))) __bf16 smem[SMEM];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // wave made provably uniform (readfirstlane): the schedule branches on it, and the K-step position (pn, ph, pw)
+    // advanced inside those branches must stay scalar — as tid >> 6 the compiler treated it as divergent, kept the
+    // position in VGPRs and wrapped every buffer load in a readfirstlane waterfall loop
+    // (h3 only, UNI: the one-term bf16 forms measured up to 18 % slower per launch this way — they keep the divergent
+    // index and the three-path loop below, profiles/r6_ab_wgrad_uniform.txt)
+    constexpr bool UNI = NT == NT_H3;
+    const int tid = threadIdx.x, lane = tid & 63, wave = UNI ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
     const int gx = Cout / 128, T = gx * 3 * (Cin / 128);
     int L;   // split-major logical order, XCD-contiguous ranges (as the per-tap kernel)
@@ -2438,30 +2444,52 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
     // loaded at the top of the step and waited out the whole HBM latency there).
     const bool early = (stg & 1) && wave >= 4;
     if ((stg & 2) && wave >= 4) __builtin_amdgcn_s_setprio(1);   // stg bit 1: the staging-first half at priority 1
-    // stg bit 2: the MFMA-first half also loads the step after next once it has staged (before the barrier, not after)
-    const bool ahead = early || (stg & 4);
+    // stg bit 2: the MFMA-first half also loads the K step after next as soon as it has staged (before the barrier; the
+    // default: loading at the top of the step after the barrier measured C2 46.16-46.26 -> 46.75-46.77 ms)
+    const bool ahead = UNI || early || (stg & 4);
     if (kt0 < kt1) { gload(); sstore(smem); }
     if (ahead && kt0 + 1 < kt1) gload();
     __syncthreads();
     int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-        const bool more = kt + 1 < kt1;
-        auto mma = [&]() { mma_at(cur); };
-        if (early) {
-            if (more) sstore(smem + (cur ^ 1) * STEP);
-            if (kt + 2 < kt1) gload();
-            mma();
-        } else if (ahead) {
-            mma();
-            if (more) sstore(smem + (cur ^ 1) * STEP);
-            if (kt + 2 < kt1) gload();
-        } else {
-            if (more) gload();
-            mma();
-            if (more) sstore(smem + (cur ^ 1) * STEP);
+    if constexpr (UNI) {
+        // one copy of the MFMAs on a single path, the staging on wave-uniform branches around it.  Round 6: with the
+        // MFMAs on three paths and the wave index divergent, the K-step position (pn, ph, pw) advanced on those paths
+        // sat in VGPRs — a readfirstlane waterfall loop around every buffer load — and the compiler shuffled the 96
+        // accumulators between register sets at every join (96 v_mov per step): C2's sums form 769 -> 685 us per launch
+        for (int kt = kt0; kt < kt1; ++kt) {
+            const bool more = kt + 1 < kt1;
+            if (early) {
+                if (more) sstore(smem + (cur ^ 1) * STEP);
+                if (kt + 2 < kt1) gload();
+            }
+            mma_at(cur);
+            if (!early) {   // (always ahead: a third load site cost 100+ register copies per step)
+                if (more) sstore(smem + (cur ^ 1) * STEP);
+                if (kt + 2 < kt1) gload();
+            }
+            __syncthreads();
+            cur ^= 1;
         }
-        __syncthreads();
-        cur ^= 1;
+    } else {
+        for (int kt = kt0; kt < kt1; ++kt) {
+            const bool more = kt + 1 < kt1;
+            auto mma = [&]() { mma_at(cur); };
+            if (early) {
+                if (more) sstore(smem + (cur ^ 1) * STEP);
+                if (kt + 2 < kt1) gload();
+                mma();
+            } else if (ahead) {
+                mma();
+                if (more) sstore(smem + (cur ^ 1) * STEP);
+                if (kt + 2 < kt1) gload();
+            } else {
+                if (more) gload();
+                mma();
+                if (more) sstore(smem + (cur ^ 1) * STEP);
+            }
+            __syncthreads();
+            cur ^= 1;
+        }
     }
     if constexpr (SUMS) {   // fold the 16 pixel rows of each channel quad (fixed order): one partial per block,
         float* red = reinterpret_cast<float*>(smem);        // [16 rows][3][128 ch] in the idle staging buffers
