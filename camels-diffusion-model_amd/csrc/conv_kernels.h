@@ -577,6 +577,42 @@ using EpiStore = EpiStoreW<2>;
 template <class EP> struct IsEpiStoreW : std::false_type {};
 template <int WM, class OT, bool ACC, bool FUSE> struct IsEpiStoreW<EpiStoreW<WM, OT, ACC, FUSE>> : std::true_type {};
 
+// EpiConvT2x2 for the transposed accumulators of gemm_deep_kernel<..., TRO = true>: acc[i][j][r] = C[m][n] at m = mw + 32 i +
+// (lane & 31), n = nw + 32 j + (r & 3) + 8 (r >> 2) + 4 (lane >> 5).  Four consecutive n (r = 4q..4q+3) are four consecutive
+// output channels of one sub-pixel ij (Co % 8 == 0: an 8-aligned column group never straddles two sub-pixels, so ij is
+// wave-uniform), stored as one float4; needs y, ldy, bias 16-byte aligned and M % 128 == N % 128 == 0 (host checks).
+struct EpiConvT2x2T {
+    float* y; long long ldy; const float* bias; int H, W, Co, M, N;
+    float* amax = nullptr;
+    __device__ __forceinline__ void operator()(f32x16 (&acc)[2][2], int mw, int nw, int lane, int, int, float*,
+                                               int) const {
+        float am = 0.f;
+        const int hw = H * W, nu = __builtin_amdgcn_readfirstlane(nw), lh = 4 * (lane >> 5);
+        float* px[2];   // the lane's input pixel m -> its output 2x2 block's first pixel
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int m = mw + 32 * i + (lane & 31), b = m / hw, rem = m - b * hw, h = rem / W, w = rem - h * W;
+            px[i] = y + ((long long)(b * 2 * H + 2 * h) * (2 * W) + 2 * w) * ldy + lh;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int nb = nu + 32 * j + 8 * q, ij = nb / Co, co = nb - ij * Co;   // wave-uniform
+                const long long off = ((long long)(ij >> 1) * (2 * W) + (ij & 1)) * ldy + co;
+                const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + co + lh) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const float4 v = make_float4(acc[i][j][4 * q] + bv.x, acc[i][j][4 * q + 1] + bv.y,
+                                                 acc[i][j][4 * q + 2] + bv.z, acc[i][j][4 * q + 3] + bv.w);
+                    *reinterpret_cast<float4*>(px[i] + off) = v;
+                    am = fmaxf(am, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+                }
+            }
+        if (amax) block_amax_commit(am, amax);
+    }
+};
+
 struct EpiConvT2x2 {  // row m = (n,h,w) input pixel, col = ij*Co + co  ->  y[n, 2h+i, 2w+j, co] = acc + b[co]
     float* y; long long ldy; const float* bias; int H, W, Co, M, N;
     float* amax = nullptr;       // optional running max|y| (block_amax_commit)
@@ -1153,7 +1189,10 @@ struct DeepConvT2x2GatherA { // the ConvT 2x2 input gradient (LdConvT2x2GatherA)
         return ((long long)(ij >> 1) * (2 * W) + (ij & 1)) * lddy + co;
     }
 };
-template <int NT, class AL, class EP, int MINB>
+// TRO (round 6): the MFMAs take B as their first operand, so each accumulator holds the tile transposed — a lane keeps one
+// row m (pixel) and, for r = 4q..4q+3, four consecutive columns n: the epilogue (EpiConvT2x2T) stores 16 bytes per
+// instruction instead of 4 (the scatter epilogue issued 64 dword stores per lane per tile, which nothing overlapped)
+template <int NT, class AL, class EP, int MINB, bool TRO = false>
 __global__ __launch_bounds__(GTHREADS, MINB) void gemm_deep_kernel(AL al, const __bf16* __restrict__ bp, int N,
                                                                   const float* amax_a, const float* amax_b, EP ep,
                                                                   int K) {
@@ -1225,21 +1264,25 @@ __global__ __launch_bounds__(GTHREADS, MINB) void gemm_deep_kernel(AL al, const 
                 fa[i][t] = *reinterpret_cast<const bf16x8*>(ab + t * XPLANE + aoff[i]);
                 fb[i][t] = *reinterpret_cast<const bf16x8*>(bb + t * XPLANE + boff[i]);
             }
+        auto mf = [&](const bf16x8& x, const bf16x8& w, const f32x16& c) {   // x: the A fragment (rows m)
+            if constexpr (TRO) return xmfma<NT>(w, x, c);
+            else return xmfma<NT>(x, w, c);
+        };
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 f32x16 c = acc[i][j];
                 if constexpr (NT >= 6) {
-                    c = xmfma<NT>(fa[i][1], fb[j][1], c);
-                    c = xmfma<NT>(fa[i][2], fb[j][0], c);
-                    c = xmfma<NT>(fa[i][0], fb[j][2], c);
+                    c = mf(fa[i][1], fb[j][1], c);
+                    c = mf(fa[i][2], fb[j][0], c);
+                    c = mf(fa[i][0], fb[j][2], c);
                 }
                 if constexpr (NT >= 3) {
-                    c = xmfma<NT>(fa[i][1], fb[j][0], c);
-                    c = xmfma<NT>(fa[i][0], fb[j][1], c);
+                    c = mf(fa[i][1], fb[j][0], c);
+                    c = mf(fa[i][0], fb[j][1], c);
                 }
-                acc[i][j] = xmfma<NT>(fa[i][0], fb[j][0], c);
+                acc[i][j] = mf(fa[i][0], fb[j][0], c);
             }
     };
     Regs R0, R1;
