@@ -2168,7 +2168,7 @@ template <int NT, int KS = 1, class PRE = PreNone, class PX = PreNone, class GT 
                                 // GT / XT: element types of dy (g and PRE's y) / of x (and PX's g): bf16 for C4's
                                 // fused-chain activations and gradients
                                 // KS: 16-pixel K steps per barrier (W % (16 KS) == 0);
-                                // KS = 2: 1.09x KS = 1 (KS = 4 needs 133 KB of LDS: the launch is refused)
+                                // KS = 2: 1.09x KS = 1; KS = 4 (133 KiB of LDS under h3): C2 -0.7 % (round 6)
                                 // PRE = PreBnBwd: dy computed from g (the dy argument) and y while staging
                                 // PX = PreBnRelu: X = relu(y s + t) computed from the previous layer's y (the x argument)
 __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restrict__ dy, int lddy, int Cout,

@@ -13,6 +13,17 @@ static int wgrad_ks4() {
     static const int v = [] { const char* e = getenv("CDM_WGRAD_KS4"); return e ? atoi(e) : 1; }();
     return v;
 }
+static int wgrad_ks1() {   // $CDM_WGRAD_KS1=1: 16-pixel K steps for the fp32-activation forms (A/B timing only)
+    static const int v = [] { const char* e = getenv("CDM_WGRAD_KS1"); return e ? atoi(e) : 0; }();
+    return v;
+}
+// 64-pixel K steps for h3 too, on the 64^2 layers ($CDM_WGRAD_KS4H3=0: 32): 133 KiB of LDS (gfx950 has 160 per CU) and
+// 254 VGPRs without spills; same-box A/B after the schedule changes, 3 rounds: C2 44.94-45.11 -> 44.66-44.78 ms
+// (profiles/r6_ab_wgrad_ks4h3.txt; 16-pixel steps: 45.70-45.77 -> 47.33-47.38, profiles/r6_ab_wgrad_ks1.txt)
+static int wgrad_ks4h3() {
+    static const int v = [] { const char* e = getenv("CDM_WGRAD_KS4H3"); return e ? atoi(e) : 1; }();
+    return v;
+}
 static int wgrad_stagger() {
     static const int v = [] { const char* e = getenv("CDM_WGRAD_STAGGER"); return e ? atoi(e) : 5; }();
     return v;
@@ -31,7 +42,14 @@ static int launch_wgrad_row(const GT* dy, int lddy, int Cout, const XT* x, int H
     const int ktiles = K / (16 * KS), per = (ktiles + sp - 1) / sp;
     dim3 grid((Cout / 128) * 3 * (Cin / 128) * ((ktiles + per - 1) / per));
     if (!F32 && nterm != 1) return (int)hipErrorInvalidValue;   // bf16 activations: the one-term (C4) arithmetic only
-    if constexpr (KS == 4) {   // 64-pixel K steps: the one-term bf16 images only (66 KiB of LDS; h3 would need 133)
+    if constexpr (KS == 4) {   // 64-pixel K steps: the one-term bf16 images (66 KiB of LDS), or h3 ($CDM_WGRAD_KS4H3: 133 KiB)
+        if constexpr (F32) {
+            if (nterm == NT_H3) {
+                hipLaunchKernelGGL((wgrad3x3_row_kernel<NT_H3, 4, PRE, PX>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H,
+                                   W, Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px, wgrad_stagger());
+                return cdm_status();
+            }
+        }
         if (nterm != 1) return (int)hipErrorInvalidValue;
         hipLaunchKernelGGL((wgrad3x3_row_kernel<1, 4, PRE, PX, GT, XT>), grid, dim3(512), 0, st, dy, lddy, Cout, x, H, W,
                            Cin, ldx, ktiles, per, amax_dy, amax_x, slab, pre, px, wgrad_stagger());
@@ -79,7 +97,7 @@ static int conv3x3_wgrad_split(const float* dy, int lddy, int Cout, const float*
     EpiStore ep{slab, NN, (long long)M * NN, nullptr, 1, 0, nullptr, 0, M, NN};
     const bool row_ok = Cin % 128 == 0 && Cout % 128 == 0 && lddy % 4 == 0 && ldx % 4 == 0;
     if ((variant == 0 || variant == 3) && row_ok) {   // kernel-row path (3 taps per block): KS = 2, else 1
-        if (variant == 0 && W % 32 == 0 && effective_splits(K, splits, 32) == sp)
+        if (variant == 0 && W % 32 == 0 && effective_splits(K, splits, 32) == sp && !wgrad_ks1())
             return launch_wgrad_row<2>(dy, lddy, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, nterm, st);
         if (W % 16 == 0 && effective_splits(K, splits, 16) == sp)
             return launch_wgrad_row<1>(dy, lddy, Cout, x, H, W, Cin, ldx, K, sp, amax_dy, amax_x, slab, nterm, st);
@@ -191,11 +209,12 @@ CDM_API int cdm_conv3x3_wgrad_x16_ex(const float* g, int ldg, const float* y, in
         (x_sums && (!x_s || !x_g || ldxg % 4 || !x_mean || !x_invstd)) || (dt && nterm != 1))
         return (int)hipErrorInvalidValue;
     const int K = N * H * W, sp = effective_splits(K, splits);
-    const bool ks2 = W % 32 == 0 && effective_splits(K, splits, 32) == sp;
+    const bool ks2 = W % 32 == 0 && effective_splits(K, splits, 32) == sp && !wgrad_ks1();
     // 64-pixel K steps for bf16 activations ($CDM_WGRAD_KS4=0: 32): with fp32 activations they measured 1.81x slower
     // per launch than 32 (1284 vs 710 us, 22 VGPRs spilled, profiles/r3_c4_ks4.txt); the bf16 staging registers are
     // half as wide (249 VGPRs, no spill): C4 29.64-29.89 -> 29.31-29.44 ms per step (profiles/r4_ab_dy_store_ks4.txt)
     const bool ks4 = wgrad_ks4() && W % 64 == 0 && effective_splits(K, splits, 64) == sp;
+    const bool ks4h3 = nterm == NT_H3 && wgrad_ks4h3() && W % 64 == 0 && effective_splits(K, splits, 64) == sp;
     if (!ks2 && effective_splits(K, splits, 16) != sp) return (int)hipErrorInvalidValue;
     const PreBnBwd pre{y, ldy, {s, t, mean, invstd, A, B, Cc}};
     const PreBnRelu px{{x_s, x_t}};
@@ -213,6 +232,8 @@ CDM_API int cdm_conv3x3_wgrad_x16_ex(const float* g, int ldg, const float* y, in
         auto wgk = [&](auto pre_, auto px_) -> int {
             if constexpr (BF) {
                 if (ks4) return CDM_WG(4, pre_, px_);
+            } else {
+                if (ks4h3) return CDM_WG(4, pre_, px_);
             }
             return ks2 ? CDM_WG(2, pre_, px_) : CDM_WG(1, pre_, px_);
         };
