@@ -391,6 +391,19 @@ CDM_API int cdm_convT2x2_dgrad_x16(const float* dy, int N, int H, int W, int Cou
         const dim3 grid(M / GBM, Cin / GBN);
         const __bf16* wb = reinterpret_cast<const __bf16*>(wx);
         const DeepConvT2x2GatherA al{dy, H, W, Cout, lddy};
+        // two resident blocks per CU ($CDM_CONVT_DGRAD_MINB=3: three): the 3-block form spills 36-50 VGPRs at its 168 cap;
+        // 199 without spill at two — bit-identical, 219 -> 209 us (h3), 203 -> 161 us (bf16) per launch, same-box trace
+        // A/B (profiles/r6_ab_convT_dgrad_minb.txt)
+        static const int mb2 = [] { const char* e = getenv("CDM_CONVT_DGRAD_MINB"); return e ? atoi(e) != 3 : 1; }();
+        if (mb2) {
+            if (nterm == NT_H3)
+                hipLaunchKernelGGL((gemm_deep_kernel<NT_H3, DeepConvT2x2GatherA, EpiStore, 2>), grid, dim3(GTHREADS), 0,
+                                   S(stream), al, wb, Cin, amax_dy, amax_w, ep, K);
+            else
+                hipLaunchKernelGGL((gemm_deep_kernel<1, DeepConvT2x2GatherA, EpiStore, 2>), grid, dim3(GTHREADS), 0,
+                                   S(stream), al, wb, Cin, amax_dy, amax_w, ep, K);
+            return cdm_status();
+        }
         if (nterm == NT_H3)
             hipLaunchKernelGGL((gemm_deep_kernel<NT_H3, DeepConvT2x2GatherA, EpiStore, 3>), grid, dim3(GTHREADS), 0,
                                S(stream), al, wb, Cin, amax_dy, amax_w, ep, K);
