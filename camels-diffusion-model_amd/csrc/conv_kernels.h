@@ -580,7 +580,7 @@ template <int WM, class OT, bool ACC, bool FUSE> struct IsEpiStoreW<EpiStoreW<WM
 // EpiConvT2x2 for the transposed accumulators of gemm_deep_kernel<..., TRO = true>: acc[i][j][r] = C[m][n] at m = mw + 32 i +
 // (lane & 31), n = nw + 32 j + (r & 3) + 8 (r >> 2) + 4 (lane >> 5).  Four consecutive n (r = 4q..4q+3) are four consecutive
 // output channels of one sub-pixel ij (Co % 8 == 0: an 8-aligned column group never straddles two sub-pixels, so ij is
-// wave-uniform), stored as one float4; needs y, ldy, bias 16-byte aligned and M % 128 == N % 128 == 0 (host checks).
+// wave-uniform), stored as one float4; needs y, ldy 16-byte aligned and M % 128 == N % 128 == 0 (host checks).
 struct EpiConvT2x2T {
     float* y; long long ldy; const float* bias; int H, W, Co, M, N;
     float* amax = nullptr;
@@ -600,7 +600,8 @@ struct EpiConvT2x2T {
             for (int q = 0; q < 4; ++q) {
                 const int nb = nu + 32 * j + 8 * q, ij = nb / Co, co = nb - ij * Co;   // wave-uniform
                 const long long off = ((long long)(ij >> 1) * (2 * W) + (ij & 1)) * ldy + co;
-                const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + co + lh) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float* bp = bias + co + lh;   // (the packed parameter buffer: not 16-byte aligned in general)
+                const float4 bv = bias ? make_float4(bp[0], bp[1], bp[2], bp[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     const float4 v = make_float4(acc[i][j][4 * q] + bv.x, acc[i][j][4 * q + 1] + bv.y,

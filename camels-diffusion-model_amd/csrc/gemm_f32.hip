@@ -332,11 +332,11 @@ CDM_API int cdm_convT2x2_fwd_x16(const float* x, int N, int H, int W, int Cin, i
         (nterm == NT_H3 || nterm == 1)) {
         const dim3 grid(M / GBM, NN / GBN);
         const __bf16* wb = reinterpret_cast<const __bf16*>(wx);
-        // transposed accumulators + 16-byte scatter stores ($CDM_CONVT_TRO=0: the dword-store epilogue) where the output
-        // rows and the bias are 16-byte aligned and a sub-pixel holds whole 8-column groups
-        static const int tro_env = [] { const char* e = getenv("CDM_CONVT_TRO"); return e ? atoi(e) : 1; }();
-        const bool tro = tro_env && Cout % 8 == 0 && ldy % 4 == 0 && reinterpret_cast<uintptr_t>(y) % 16 == 0 &&
-                         (!bias || reinterpret_cast<uintptr_t>(bias) % 16 == 0);
+        // transposed accumulators + 16-byte scatter stores ($CDM_CONVT_TRO=1; needs 16-byte aligned output rows and
+        // whole 8-column groups per sub-pixel): bit-identical but 213 -> 219 us per launch in the sampling step and C2
+        // +0.15 ms (profiles/r6_ab_convT_tro.txt) — the dword-store epilogue was not store-issue bound; off
+        static const int tro_env = [] { const char* e = getenv("CDM_CONVT_TRO"); return e ? atoi(e) : 0; }();
+        const bool tro = tro_env && Cout % 8 == 0 && ldy % 4 == 0 && reinterpret_cast<uintptr_t>(y) % 16 == 0;
         if (tro) {
             const EpiConvT2x2T et{y, ldy, bias, H, W, Cout, M, NN, amax_y};
             if (nterm == NT_H3)
