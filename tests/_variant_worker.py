@@ -1,7 +1,9 @@
 """Child process of tests/test_gpu_kernels.py::test_deep_staging_bit_exact: runs the bf16 forward halo conv, whose
 staging schedule an environment switch selects ($CDM_HALO_DEEP, read once per process by the library), the fused
 weight gradients, and the C_in = 1 forward / C_out = 1 input gradient (row or flat-pixel kernels: $CDM_ROW_KERNELS) on
-fixed seeded inputs and saves their outputs, so the test can compare two processes bit for bit.
+fixed seeded inputs and saves their outputs, so the test can compare two processes bit for bit.  Round 6 adds the
+schedule switches $CDM_WGRAD_STAGGER, $CDM_HALO_BEARLY and $CDM_CONVT_DGRAD_MINB (the weight gradient with the producer
+BN sums, the h3 halo forward, the h3 ConvT input gradient).
 
     python tests/_variant_worker.py OUT.pt
 """
@@ -55,6 +57,53 @@ def main(out_path):
                                               None, None, None, am.data_ptr(), am.data_ptr() + 4, sp, slab.data_ptr(),
                                               nterm, 0, s) == 0
             out[f"wgrad_{nterm}_{S}"] = slab.cpu()
+    # round 6 schedules: the row weight gradient with the producer BN sums (64-pixel K steps under h3 at 64^2; staggered
+    # look-ahead order vs lock-step, $CDM_WGRAD_STAGGER), the h3 halo forward (B one kernel row earlier,
+    # $CDM_HALO_BEARLY), the h3 ConvT 2x2 input gradient (two vs three blocks per CU, $CDM_CONVT_DGRAD_MINB)
+    for nterm in (4, 1):
+        B, S, ci, co = 4, 64, 128, 128
+        P = B * S * S
+        yx = torch.randn(P, ci, device="cuda", generator=g)
+        gx = torch.randn(P, ci, device="cuda", generator=g)
+        dyy = torch.randn(P, co, device="cuda", generator=g) * 1e-2
+        xs_, xt_ = torch.rand(ci, device="cuda", generator=g) + 0.5, torch.randn(ci, device="cuda", generator=g) * 0.1
+        mu, inv = torch.randn(ci, device="cuda", generator=g) * 0.1, torch.rand(ci, device="cuda", generator=g) + 0.5
+        am = torch.ones(4, device="cuda") * 8.0
+        sp = wgrad_splits(P, co, 9 * ci)
+        slab = torch.empty(sp * co * 9 * ci, device="cuda")
+        sums = torch.empty(sp * 3 * (co // 128) * 5 * ci, device="cuda")
+        assert L.cdm_conv3x3_wgrad_x16_ex(dyy.data_ptr(), co, None, 0, None, None, None, None, None, None, None, co,
+                                          yx.data_ptr(), B, S, S, ci, ci, xs_.data_ptr(), xt_.data_ptr(), gx.data_ptr(),
+                                          ci, mu.data_ptr(), inv.data_ptr(), sums.data_ptr(), am.data_ptr(),
+                                          am.data_ptr() + 4, sp, slab.data_ptr(), nterm, 0, s) == 0
+        out[f"wgrad_sums_{nterm}"], out[f"wgrad_sums_sums_{nterm}"] = slab.cpu(), sums.cpu()
+    N, H, C = 5, 64, 128
+    P = N * H * H
+    xh = torch.randn(P, C, device="cuda", generator=g).relu()
+    wpk = torch.empty(9 * C, C, device="cuda")
+    Wh, bh = torch.randn(C, C, 3, 3, device="cuda", generator=g) * 0.05, torch.randn(C, device="cuda", generator=g)
+    L.cdm_pack_conv3x3(Wh.data_ptr(), bh.data_ptr(), C, C, None, None, None, None, 0.0, wpk.data_ptr(), None, None, 16, s)
+    amh = torch.zeros(2, device="cuda")
+    L.cdm_amax_f32(wpk.data_ptr(), 9 * C, C, C, amh.data_ptr() + 4, 0, s)
+    L.cdm_amax_f32(xh.data_ptr(), P, C, C, amh.data_ptr(), 0, s)
+    wxh = torch.empty(9 * C // 16 * 3 * C * 16, dtype=torch.bfloat16, device="cuda")
+    L.cdm_split_f16x2(wpk.data_ptr(), C, 9 * C, C, amh.data_ptr() + 4, wxh.data_ptr(), s)
+    yh, sth = torch.empty(P, C, device="cuda"), torch.empty((P + 127) // 128, 2, C, device="cuda")
+    assert L.cdm_conv3x3_fwd_h3(xh.data_ptr(), N, H, H, C, C, wxh.data_ptr(), amh.data_ptr(), amh.data_ptr() + 4, None,
+                                yh.data_ptr(), C, C, 0, sth.data_ptr(), C, 16, None, s) == 0
+    out["halo_h3_y"], out["halo_h3_stats"] = yh.cpu(), sth.cpu()
+    N, H, Co, Ci = 2, 32, 128, 256                       # ConvT input grid H x H, its output channels Co
+    dyt = torch.randn(N * 4 * H * H, Co, device="cuda", generator=g)
+    wt = torch.randn(4 * Co, Ci, device="cuda", generator=g) * 0.05
+    amt = torch.zeros(2, device="cuda")
+    L.cdm_amax_f32(dyt.data_ptr(), N * 4 * H * H, Co, Co, amt.data_ptr(), 0, s)
+    L.cdm_amax_f32(wt.data_ptr(), 4 * Co, Ci, Ci, amt.data_ptr() + 4, 0, s)
+    wxt = torch.empty(4 * Co // 16 * 3 * Ci * 16, dtype=torch.bfloat16, device="cuda")
+    L.cdm_split_f16x2(wt.data_ptr(), Ci, 4 * Co, Ci, amt.data_ptr() + 4, wxt.data_ptr(), s)
+    dxt = torch.empty(N * H * H, Ci, device="cuda")
+    assert L.cdm_convT2x2_dgrad_x16(dyt.data_ptr(), N, H, H, Co, Co, wxt.data_ptr(), amt.data_ptr(),
+                                    amt.data_ptr() + 4, dxt.data_ptr(), Ci, Ci, 0, 4, s) == 0
+    out["convT_dgrad_h3"] = dxt.cpu()
     # C_in = 1 forward and C_out = 1 input gradient: the row kernels vs the flat-pixel kernels ($CDM_ROW_KERNELS)
     for (N, H, W, C) in ((3, 64, 64, 128), (2, 32, 32, 256), (2, 24, 40, 64), (1, 256, 256, 128)):
         x1 = torch.randn(N * H * W, device="cuda", generator=g)

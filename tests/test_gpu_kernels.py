@@ -502,7 +502,10 @@ def test_deep_staging_bit_exact(L, tmp_path):
     """The two-deep staging schedule of the bf16 forward halo conv (the halo two chunks ahead, $CDM_HALO_DEEP) produces
     the one-ahead schedule's output bit for bit, the row forms of the C_in = 1 forward and C_out = 1 input gradient equal
     the flat-pixel kernels bit for bit ($CDM_ROW_KERNELS), and the fused weight gradients are reproducible across
-    processes: two child processes (tests/_variant_worker.py), the library reading the switches once per process."""
+    processes: two child processes (tests/_variant_worker.py), the library reading the switches once per process.
+    Round 6: the second process also runs the previous schedules — the lock-step weight gradient ($CDM_WGRAD_STAGGER=0),
+    the halo B fetched in the last kernel row ($CDM_HALO_BEARLY=0), the ConvT input gradient at three blocks per CU
+    ($CDM_CONVT_DGRAD_MINB=3) — which must give the same bits (slabs, producer BN sums, outputs, statistics)."""
     import subprocess
     import sys
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_variant_worker.py")
@@ -510,6 +513,8 @@ def test_deep_staging_bit_exact(L, tmp_path):
     for deep in ("1", "0"):
         f = tmp_path / f"deep{deep}.pt"
         env = dict(os.environ, CDM_HALO_DEEP=deep, CDM_ROW_KERNELS=deep)
+        if deep == "0":
+            env.update(CDM_WGRAD_STAGGER="0", CDM_HALO_BEARLY="0", CDM_CONVT_DGRAD_MINB="3")
         r = subprocess.run([sys.executable, worker, str(f)], env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(torch.load(f))
