@@ -2188,9 +2188,12 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_row_kernel(const GT* __restri
     // wave made provably uniform (readfirstlane): the schedule branches on it, and the K-step position (pn, ph, pw)
     // advanced inside those branches must stay scalar — as tid >> 6 the compiler treated it as divergent, kept the
     // position in VGPRs and wrapped every buffer load in a readfirstlane waterfall loop
-    // (h3 only, UNI: the one-term bf16 forms measured up to 18 % slower per launch this way — they keep the divergent
-    // index and the three-path loop below, profiles/r6_ab_wgrad_uniform.txt)
-    constexpr bool UNI = NT == NT_H3;
+    // UNI per form, as measured (profiles/r6_ab_wgrad_uniform.txt, r6_ab_wgrad_uniform_bf16.txt): h3, and the one-term
+    // forms with the producer sums (both operand types alike, or 32-pixel steps) or 64-pixel steps without them (-2 to
+    // -7 % per launch); the other one-term forms keep the divergent index and the three-path loop below (+6 to +24 %
+    // with the uniform one)
+    constexpr bool SUMSF = PX::kind == 3;
+    constexpr bool UNI = NT == NT_H3 || (SUMSF && (std::is_same<GT, XT>::value || KS == 2)) || (!SUMSF && KS == 4);
     const int tid = threadIdx.x, lane = tid & 63, wave = UNI ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
     const int gx = Cout / 128, T = gx * 3 * (Cin / 128);
