@@ -1448,7 +1448,6 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
     // ticks (halo_delay: desynchronises the blocks' epilogue store bursts)
     const int stg = stgd & 1;
     const bool bearly = (stgd & 4) != 0;   // stgd bit 2: the three-barrier schedule fetches B one group earlier
-    const bool hsplit = (stgd & 16) != 0 && !(ABL & 1024);   // stgd bit 4: the next halo staged over two kernel rows
     constexpr int NS = XTerms<NT>::NS;
     // TALL (ABL 8192, one bf16 term only): 4 waves (one per SIMD, 512 registers each: the accumulators live in AGPRs) as
     // 2 (M) x 2 (N) of 128 x 64 — 4 row blocks of 32 pixels per wave.  The one-term MFMA reads 1 KiB of fragments per
@@ -1588,7 +1587,7 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
         }
     };
     // inb(j): piece j lies inside the image (else zero padding)
-    auto store_halo_impl = [&](const RawX (&src)[HQ], auto inb, __bf16* base, int cc, int j0 = 0, int j1 = 1 << 30) {
+    auto store_halo_impl = [&](const RawX (&src)[HQ], auto inb, __bf16* base, int cc) {
         float cf[NCOEF ? NCOEF : 1][4];   // coefficients of this thread's 4 channels (q & 3 == tid & 3 for every j)
         if constexpr (NCOEF > 0) {
             const int cb = cc * 16 + (tid & 3) * 4;
@@ -1600,7 +1599,6 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
         }
 #pragma unroll
         for (int j = 0; j < HQ; ++j) {
-            if (j < j0 || j >= j1) continue;   // (a piece range: constants at every call site)
             if (HPAD || hdst[j] >= 0) {
                 const float4 sv = Act<XT>::to4(src[j]);
                 float xv[4] = {sv.x, sv.y, sv.z, sv.w};
@@ -1642,9 +1640,7 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
             }
         }
     };
-    auto store_halo = [&](__bf16* base, int cc, int j0 = 0, int j1 = 1 << 30) {
-        store_halo_impl(hreg, [&](int j) { return hin[j]; }, base, cc, j0, j1);
-    };
+    auto store_halo = [&](__bf16* base, int cc) { store_halo_impl(hreg, [&](int j) { return hin[j]; }, base, cc); };
     auto store_halo_set = [&](const RawX (&src)[HQ], unsigned mask, __bf16* base, int cc) {
         store_halo_impl(src, [&](int j) { return ((mask >> j) & 1u) != 0u; }, base, cc);
     };
@@ -1914,12 +1910,7 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
         // dy = 1 (bearly: B of the next chunk's dy = 0 fetched here, into the register set stored in dy = 0, so it has a
         // whole group's MFMAs to arrive instead of being stored right after the MFMAs it was issued before)
         if (bearly) gload_b(morec ? g0 + 3 : 0, bregA);
-        // hsplit: the first half of the next chunk's halo pieces split + stored in this kernel row (its buffer is idle
-        // since chunk cc-1), the rest in the last one, so the two rows carry the staging VALU evenly
-        const bool late1 = wave < NTH / 128;
-        if (hsplit && morec && !late1) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1, 0, HQ / 2);
         compute(1, a, Bs + bb * BPL * XPLANE, V0{});
-        if (hsplit && morec && late1) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1, 0, HQ / 2);
         store_b((bb ^ 1) * BPL * XPLANE, bregB);
         sync();
         bb ^= 1;
@@ -1930,9 +1921,8 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
         // after this kernel row's MFMAs, waves 4-7 before them, so each SIMD pairs one wave's VALU with its partner's
         // MFMAs (wave-uniform)
         const bool late = ((ABL & 256) || stg) && wave < NTH / 128;
-        const int hj0 = hsplit ? HQ / 2 : 0;
         if constexpr (!(ABL & 1024)) {
-            if (morec && !late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1, hj0, HQ);
+            if (morec && !late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
         }
         compute(2, a, Bs + bb * BPL * XPLANE, VH{});
         if constexpr (ABL & 1024) {
@@ -1941,7 +1931,7 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
             // the idle buffer, which the next tile's chunk 0 overwrites after the epilogue
             store_halo(Hs + (hb ^ 1) * NS * HPLANE, morec ? cc + 1 : 0);
         }
-        if (morec && late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1, hj0, HQ);
+        if (morec && late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
         if (morec) store_b((bb ^ 1) * BPL * XPLANE, bregA);
         sync();
         bb ^= 1;
@@ -2619,10 +2609,7 @@ static int halo_stagger(int nterm) {   // default on for h3 and (round 4, profil
     // profiles/r6_ab_halo_bearly.txt)
     static const int p = [] { const char* e = getenv("CDM_HALO_PRIO"); return e ? atoi(e) : 0; }();
     static const int be = [] { const char* e = getenv("CDM_HALO_BEARLY"); return e ? atoi(e) : 1; }();
-    // + the next chunk's halo staged over the last two kernel rows (bit 4; $CDM_HALO_HSPLIT)
-    static const int hs = [] { const char* e = getenv("CDM_HALO_HSPLIT"); return e ? atoi(e) : 0; }();
-    return (v >= 0 ? v : ((nterm == NT_H3 || nterm == 1) ? 1 : 0)) | (p ? 2 : 0) | (be ? 4 : 0) | (hs ? 16 : 0) |
-           (d << 8);
+    return (v >= 0 ? v : ((nterm == NT_H3 || nterm == 1) ? 1 : 0)) | (p ? 2 : 0) | (be ? 4 : 0) | (d << 8);
 }
 
 // the one-barrier-per-chunk schedule of the one-term (bf16) LDS-halo conv ($CDM_HALO_ONEB=0: three barriers per chunk)
