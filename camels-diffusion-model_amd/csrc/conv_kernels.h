@@ -1447,7 +1447,7 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
     // every other block in 10 ns
     // ticks (halo_delay: desynchronises the blocks' epilogue store bursts)
     const int stg = stgd & 1;
-    const bool bearly = (stgd & 4) != 0;   // stgd bit 2: the three-barrier schedule fetches B one group earlier
+    constexpr bool bearly = true;   // B of the next chunk's first kernel row fetched in row 1 (round 6, profiles/r6_ab_halo_bearly.txt)
     constexpr int NS = XTerms<NT>::NS;
     // TALL (ABL 8192, one bf16 term only): 4 waves (one per SIMD, 512 registers each: the accumulators live in AGPRs) as
     // 2 (M) x 2 (N) of 128 x 64 — 4 row blocks of 32 pixels per wave.  The one-term MFMA reads 1 KiB of fragments per
@@ -1909,14 +1909,14 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
         bb ^= 1;
         // dy = 1 (bearly: B of the next chunk's dy = 0 fetched here, into the register set stored in dy = 0, so it has a
         // whole group's MFMAs to arrive instead of being stored right after the MFMAs it was issued before)
-        if (bearly) gload_b(morec ? g0 + 3 : 0, bregA);
+        if constexpr (bearly) gload_b(morec ? g0 + 3 : 0, bregA);
         compute(1, a, Bs + bb * BPL * XPLANE, V0{});
         store_b((bb ^ 1) * BPL * XPLANE, bregB);
         sync();
         bb ^= 1;
         // dy = 2: fetch B of the next chunk's dy = 0; split + store the next halo (buffer idle since chunk cc-1)
         // ahead of this group's MFMAs, so its VALU work interleaves with them; B after them (just issued)
-        if (!bearly) gload_b(morec ? g0 + 3 : 0, bregA);
+        if constexpr (!bearly) gload_b(morec ? g0 + 3 : 0, bregA);
         // staggered split (ABL 256, or stg at run time: $CDM_HALO_STAGGER): waves 0-3 split + store the next halo
         // after this kernel row's MFMAs, waves 4-7 before them, so each SIMD pairs one wave's VALU with its partner's
         // MFMAs (wave-uniform)
@@ -2603,13 +2603,13 @@ static int halo_stagger(int nterm) {   // default on for h3 and (round 4, profil
     static const int v = [] { const char* e = getenv("CDM_HALO_STAGGER"); return e ? atoi(e) : -1; }();
     // + the block start delay (bits 8+, 10 ns ticks; $CDM_HALO_DELAY)
     static const int d = [] { const char* e = getenv("CDM_HALO_DELAY"); return e ? atoi(e) : 0; }();
-    // + static priority 1 for waves 4-7 (bit 1; $CDM_HALO_PRIO, measured neutral: off, profiles/r6_ab_wave_priority.txt),
-    // B fetched one group earlier (bit 2; $CDM_HALO_BEARLY, on: bit-identical, same-box A/B sampling 13.37-13.40 ->
-    // 13.15-13.18 ms per step (w = 0), 26.31-26.36 -> 25.89-25.96 (w = 3), C2 train 47.20-47.25 -> 47.09-47.13 ms,
-    // profiles/r6_ab_halo_bearly.txt)
+    // + static priority 1 for waves 4-7 (bit 1; $CDM_HALO_PRIO, measured neutral: off, profiles/r6_ab_wave_priority.txt).
+    // (B fetched one kernel row earlier is compiled in since round 6: as a runtime switch, bit 2, it had measured
+    // sampling 13.37-13.40 -> 13.15-13.18 ms per step, profiles/r6_ab_halo_bearly.txt; as a constant a further 13.08-13.20
+    // -> 12.87-12.95 and C2 45.10-45.31 -> 44.72-44.83 ms, profiles/r6_ab_halo_bearly_const.txt — the switch's second
+    // load site and its branches had cost that much)
     static const int p = [] { const char* e = getenv("CDM_HALO_PRIO"); return e ? atoi(e) : 0; }();
-    static const int be = [] { const char* e = getenv("CDM_HALO_BEARLY"); return e ? atoi(e) : 1; }();
-    return (v >= 0 ? v : ((nterm == NT_H3 || nterm == 1) ? 1 : 0)) | (p ? 2 : 0) | (be ? 4 : 0) | (d << 8);
+    return (v >= 0 ? v : ((nterm == NT_H3 || nterm == 1) ? 1 : 0)) | (p ? 2 : 0) | (d << 8);
 }
 
 // the one-barrier-per-chunk schedule of the one-term (bf16) LDS-halo conv ($CDM_HALO_ONEB=0: three barriers per chunk)
