@@ -1921,29 +1921,35 @@ __global__ __launch_bounds__((ABL & 8192) ? 256 : HTHREADS, 1) void conv3x3_halo
         // after this kernel row's MFMAs, waves 4-7 before them, so each SIMD pairs one wave's VALU with its partner's
         // MFMAs (wave-uniform)
         const bool late = ((ABL & 256) || stg) && wave < NTH / 128;
+        // (round 6) after the block's last chunk these stores write the next tile's chunk 0 (halo and B, fetched during
+        // this chunk; setup_tile moved the halo offsets) into the buffers its first chunk reads — the work the post-loop
+        // stores did — so the stores need no `more chunks` condition (each condition was one more basic block splitting
+        // the MFMAs' scheduling region; after the last tile they rewrite idle buffers)
+        const int cn = morec ? cc + 1 : 0;
         if constexpr (!(ABL & 1024)) {
-            if (morec && !late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
+            if (!late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cn);
         }
         compute(2, a, Bs + bb * BPL * XPLANE, VH{});
         if constexpr (ABL & 1024) {
             // after the MFMAs in program order (its LDS writes may alias the fragment reads) but in their scheduling
-            // region: the split's VALU fills the MFMA gaps; unconditional — after the block's last chunk it writes
-            // the idle buffer, which the next tile's chunk 0 overwrites after the epilogue
-            store_halo(Hs + (hb ^ 1) * NS * HPLANE, morec ? cc + 1 : 0);
+            // region: the split's VALU fills the MFMA gaps
+            store_halo(Hs + (hb ^ 1) * NS * HPLANE, cn);
         }
-        if (morec && late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cc + 1);
-        if (morec) store_b((bb ^ 1) * BPL * XPLANE, bregA);
+        if (late) store_halo(Hs + (hb ^ 1) * NS * HPLANE, cn);
+        store_b((bb ^ 1) * BPL * XPLANE, bregA);
         sync();
         bb ^= 1;
         hb ^= 1;
     }
     }
     if constexpr (!TALL) unscale<NT>(acc, sx, op_scale<NT>(amax_w));   // (one term: unscaled)
-    if (!DEEP && nextt) {   // the next tile's chunk 0 (its loads were issued during the last chunk) into the halo / B buffers
-        // idle since the last chunk's closing barrier, ahead of the epilogue: its prefetch registers die before the
-        // epilogue and the epilogue needs no barrier pair after it
-        store_halo(Hs + hb * NS * HPLANE, 0);
-        store_b(bb * BGR * BPL * XPLANE, bregA);
+    if constexpr (ONEB && !DEEP) {   // (the three-barrier schedule stored them in its last kernel row)
+        if (nextt) {   // the next tile's chunk 0 (its loads were issued during the last chunk) into the halo / B buffers
+            // idle since the last chunk's closing barrier, ahead of the epilogue: its prefetch registers die before the
+            // epilogue and the epilogue needs no barrier pair after it
+            store_halo(Hs + hb * NS * HPLANE, 0);
+            store_b(bb * BGR * BPL * XPLANE, bregA);
+        }
     }
     // epilogue scratch (stats / max-min: 4 KiB): the other halo buffer (>= 24 KiB), last read by the final chunk
     // before its closing barrier
